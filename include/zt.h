@@ -1,0 +1,133 @@
+/*
+ * zt.h -- C-ABI of the MI355X-native DEFLATE engine (libzt.so).
+ *
+ * Drop-in boundary for ExaGraphica/zlib.ts's hot path.  Every entry point is
+ * plain C (pointers + sizes, no torch/HIP types), synchronous, and computes on
+ * the GPU; there is no CPU fallback -- without a usable HIP device the calls
+ * return ZT_E_NO_DEVICE.  The N-API addon (zlib.ts_amd/native/zt_napi.cc)
+ * binds these for the JS facade that keeps the reference's class shapes.
+ *
+ * Each function names the reference interface it replaces (path:line in
+ * ExaGraphica/zlib.ts @ 2024-10-08).  Error codes map 1:1 onto the
+ * reference's thrown messages; zt_last_error_message() returns the exact text.
+ */
+#ifndef ZT_H
+#define ZT_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ------------------------------------------------------ */
+#define ZT_OK 0
+#define ZT_E_INVALID_COMPRESSION_TYPE -1 /* 'invalid compression type'  src/RawDeflate.ts:110 */
+#define ZT_E_INVALID_INDEX -2            /* Error('invalid index')      src/Bitstream.ts:29   */
+#define ZT_E_INPUT_BROKEN -10            /* 'input buffer is broken'    src/RawInflate.ts:188,282 */
+#define ZT_E_INVALID_CODE_LENGTH -11     /* 'invalid code length: N'    src/RawInflate.ts:238 */
+#define ZT_E_UNKNOWN_BTYPE -12           /* 'unknown BTYPE: N'          src/RawInflate.ts:168 */
+#define ZT_E_STORED_LEN -13              /* '...uncompressed block header: LEN'  :266 */
+#define ZT_E_STORED_NLEN -14             /* '...uncompressed block header: NLEN' :272 */
+#define ZT_E_INVALID_DISTANCE -15        /* RFC 1951 violation the reference does not check (:507) */
+#define ZT_E_INVALID_SYMBOL -16          /* lit/len 286-287 or dist 30-31 used (RFC 1951 3.2.6) */
+#define ZT_E_BAD_TREE -17                /* over-subscribed / empty code-length set */
+#define ZT_E_NO_DEVICE -100              /* no HIP device: the engine never falls back to the CPU */
+#define ZT_E_HIP -101                    /* HIP runtime failure (see message) */
+#define ZT_E_NOMEM -102
+#define ZT_E_ARG -103
+
+/* ---- devices ----------------------------------------------------------- */
+int zt_device_count(void);
+/* Select the device used by the calling thread (default 0). */
+int zt_set_device(int device);
+/* Text of the last error on this thread, formatted like the reference's
+ * message (e.g. "invalid code length: 9"). */
+const char *zt_last_error_message(void);
+/* Library version string. */
+const char *zt_version(void);
+/* Free a buffer returned by the library. */
+void zt_free(void *p);
+
+/* ---- checksums (host pointers) ------------------------------------------ */
+/* Replaces CRC32.update(data, crc, pos, length)  src/CRC32.ts:25-47 (and
+ * CRC32.create, :13-15, with crc = 0).  Result in *out (unsigned, >>> 0). */
+int zt_crc32_update(uint32_t crc, const uint8_t *data, size_t len, uint32_t *out);
+/* Replaces Adler32.update(adler, array, len, pos)  src/Adler32.ts:28-48 (and
+ * Adler32.create, :13-20, with adler = 1). */
+int zt_adler32_update(uint32_t adler, const uint8_t *data, size_t len, uint32_t *out);
+/* Both checksums in one read of the data (the GZip/Zip/zlib containers call
+ * CRC32/Adler32 beside RawDeflate: src/GZip.ts:180, src/Deflate.ts:81). */
+int zt_checksums(const uint8_t *data, size_t len, uint32_t crc_in, uint32_t adler_in, uint32_t *crc_out,
+                 uint32_t *adler_out);
+
+/* ---- raw DEFLATE (RFC 1951) ---------------------------------------------- */
+typedef struct {
+  int compression_type; /* RawDeflateOptions.compressionType: 0 NONE, 1 FIXED, 2 DYNAMIC (default 2) */
+  int lazy;             /* RawDeflateOptions.lazy (reference semantics: defer matches shorter than this) */
+  int level;            /* engine extension: 1..9, 0 = store; default (-1) = 6 */
+} zt_deflate_opts;
+
+/* Replaces new RawDeflate(input, opts).compress()  src/RawDeflate.ts:67-114.
+ * *out (free with zt_free) receives a complete raw DEFLATE stream of *out_len
+ * bytes: a valid RFC 1951 stream that the reference RawInflate decodes to
+ * `in` bit-exactly.  (The outputBuffer/outputIndex prefix handling of the
+ * reference lives in the facade.)  opts may be NULL. */
+int zt_deflate_raw(const uint8_t *in, size_t n, const zt_deflate_opts *opts, uint8_t **out, size_t *out_len);
+
+typedef struct {
+  int buffer_type; /* RawInflateOptions.bufferType (0 BLOCK, 1 ADAPTIVE); accepted, output identical */
+  size_t buffer_size; /* RawInflateOptions.bufferSize; accepted (capacity is not observable) */
+  int ref_strict;  /* 1: also fail where the reference's over-strict readBits EOF check
+                      (src/RawInflate.ts:187) throws 'input buffer is broken' on a valid stream */
+} zt_inflate_opts;
+
+/* Replaces new RawInflate(input, {index}).decompress()  src/RawInflate.ts:104-140.
+ * Decodes the stream that starts at in[index].  *end_ip receives the
+ * reference's .ip after decompress (byte just past the last used bit).
+ * opts may be NULL. */
+int zt_inflate_raw(const uint8_t *in, size_t n, size_t index, const zt_inflate_opts *opts, uint8_t **out,
+                   size_t *out_len, size_t *end_ip);
+
+/* Batch forms: `count` independent buffers in one launch (config C2/C4).
+ * status[i] receives each item's code; the call returns the first failure. */
+int zt_inflate_raw_batch(const uint8_t *const *in, const size_t *n, size_t count, const zt_inflate_opts *opts,
+                         uint8_t **out, size_t *out_len, size_t *end_ip, int *status);
+int zt_deflate_raw_batch(const uint8_t *const *in, const size_t *n, size_t count, const zt_deflate_opts *opts,
+                         uint8_t **out, size_t *out_len, int *status);
+
+/* ---- device-resident forms (inputs already in HBM; used by bench.py) ------ */
+/* `stream` is a hipStream_t (NULL = the library's stream for this device).
+ * Pointers are device pointers of the current device.  They enqueue work and
+ * return; results written to device memory are valid after the stream syncs,
+ * host outputs (sizes) are valid on return. */
+int zt_dev_checksums(const void *d_in, size_t n, uint32_t crc_in, uint32_t adler_in, uint32_t *crc_out,
+                     uint32_t *adler_out, void *stream);
+
+typedef struct zt_deflate_plan zt_deflate_plan;
+/* Workspace for deflating up to max_n bytes (chunk scratch, token buffers). */
+int zt_deflate_plan_create(size_t max_n, const zt_deflate_opts *opts, zt_deflate_plan **plan);
+void zt_deflate_plan_destroy(zt_deflate_plan *plan);
+/* Upper bound on the compressed size of n bytes. */
+size_t zt_deflate_bound(size_t n);
+/* Deflate d_in[0..n) into d_out (capacity zt_deflate_bound(n)); writes the
+ * stream length to *out_len (host).  When final == 0 the stream is left open
+ * (ends on a byte-aligned sync point, no BFINAL) so shards can be
+ * concatenated; `halo` bytes before d_in (d_in - halo .. d_in) are used as
+ * the match window of the first chunk (multi-GPU shards). */
+int zt_deflate_dev(zt_deflate_plan *plan, const void *d_in, size_t n, size_t halo, int final, void *d_out,
+                   size_t *out_len, void *stream);
+
+typedef struct zt_inflate_plan zt_inflate_plan;
+int zt_inflate_plan_create(size_t max_in, size_t max_out, zt_inflate_plan **plan);
+void zt_inflate_plan_destroy(zt_inflate_plan *plan);
+/* Inflate the raw stream d_in[0..n) into d_out (capacity out_cap).  Streams
+ * with byte-aligned sync points (empty stored blocks, as zt_deflate_dev and
+ * zlib Z_SYNC_FLUSH emit) are decoded chunk-parallel. */
+int zt_inflate_dev(zt_inflate_plan *plan, const void *d_in, size_t n, void *d_out, size_t out_cap,
+                   size_t *out_len, size_t *end_ip, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,286 @@
+// checksum.hip -- CRC-32 and Adler-32 over device-resident bytes, fused in
+// one HBM pass (replaces src/CRC32.ts:25-47 and src/Adler32.ts:28-48).
+//
+// Decomposition (HBM-bound byte work; no MFMA):
+//   * the input is cut into 256 KiB segments, one workgroup each (grid-stride);
+//   * each of the 256 threads owns one contiguous 1 KiB slice and streams it as
+//     8 lines of 128 B (eight 16-B loads per line, issued together, so a line is
+//     fetched once into L1 and fully consumed by its lane);
+//   * CRC: slice-by-8 with 16 nibble tables, each replicated 32x in LDS so that
+//     lane l always reads bank l -- every ds_read_b32 is conflict-free
+//     (2 lookups/byte);  Adler: v_dot4_u32_u8 weighted sums, 10 VALU / 16 B;
+//   * per-slice results are merged with polynomial shifts (CRC) and weighted
+//     sums (Adler) inside the workgroup, then one tiny kernel merges segments.
+// Algorithmic bytes per unit: N input bytes read.
+#include "zt_internal.h"
+
+namespace zt {
+
+namespace {
+
+constexpr int CK_THREADS = 256;
+constexpr int CK_SLICE = 1024;                       // bytes per thread
+constexpr size_t CK_SEG = (size_t)CK_THREADS * CK_SLICE;  // 256 KiB per segment
+constexpr int NIB_ENTRIES = 16 * 16;                 // 16 nibble positions x 16 values
+
+struct SegResult {
+  uint32_t crc;   // raw CRC register (init 0, no final xor) over the segment's bytes
+  uint32_t len;   // valid bytes in the segment
+  uint32_t s1;    // Adler sums mod 65521 (init 0)
+  uint32_t s2;
+};
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint4 ld_stream(const uint4 *p) {
+  u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+__device__ __forceinline__ uint32_t lut(const uint32_t *T, int pos, uint32_t nib, int lane) {
+  return T[(((pos << 4) + nib) << 5) + lane];
+}
+
+// One 8-byte CRC step: state xors into the first 4 bytes (reflected slice-by-8).
+__device__ __forceinline__ uint32_t crc_step8(uint32_t c, uint32_t w0, uint32_t w1, const uint32_t *T, int lane) {
+  uint32_t a = c ^ w0;
+  uint32_t r = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r ^= lut(T, j, (a >> (4 * j)) & 15u, lane);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r ^= lut(T, 8 + j, (w1 >> (4 * j)) & 15u, lane);
+  return r;
+}
+
+__device__ __forceinline__ uint32_t crc_byte(uint32_t c, uint32_t b) {
+  c ^= b;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ ZT_CRC_POLY : c >> 1;
+  return c;
+}
+
+// Adler over one 16-byte piece: s2 += 16*s1 + weighted(piece); s1 += sum(piece)
+__device__ __forceinline__ void adler16(uint32_t &s1, uint32_t &s2, uint4 v) {
+  uint32_t w = __builtin_amdgcn_udot4(v.x, 0x0D0E0F10u, 0u, false);
+  w = __builtin_amdgcn_udot4(v.y, 0x090A0B0Cu, w, false);
+  w = __builtin_amdgcn_udot4(v.z, 0x05060708u, w, false);
+  w = __builtin_amdgcn_udot4(v.w, 0x01020304u, w, false);
+  uint32_t s = __builtin_amdgcn_udot4(v.x, 0x01010101u, 0u, false);
+  s = __builtin_amdgcn_udot4(v.y, 0x01010101u, s, false);
+  s = __builtin_amdgcn_udot4(v.z, 0x01010101u, s, false);
+  s = __builtin_amdgcn_udot4(v.w, 0x01010101u, s, false);
+  s2 += (s1 << 4) + w;
+  s1 += s;
+}
+
+template <bool DO_CRC, bool DO_ADLER>
+__global__ __launch_bounds__(CK_THREADS) void checksum_segments(const uint8_t *__restrict__ frame, size_t lo,
+                                                                 size_t hi, size_t nseg,
+                                                                 const uint32_t *__restrict__ nib_g,
+                                                                 const uint32_t *__restrict__ x2n_g,
+                                                                 SegResult *__restrict__ out) {
+  // 32 KiB of replicated nibble tables + the combine scratch
+  __shared__ uint32_t T[DO_CRC ? NIB_ENTRIES * 32 : 1];
+  __shared__ uint32_t x2n[32];
+  __shared__ uint32_t red_c[CK_THREADS];
+  __shared__ uint32_t red_l[CK_THREADS];
+  __shared__ unsigned long long red_a[CK_THREADS / 64][2];
+
+  const int tid = threadIdx.x;
+  const int lane32 = tid & 31;
+  if (DO_CRC) {
+    for (int i = tid; i < NIB_ENTRIES * 32; i += CK_THREADS) T[i] = nib_g[i >> 5];
+    if (tid < 32) x2n[tid] = x2n_g[tid];
+  }
+  __syncthreads();
+
+  for (size_t seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
+    const size_t seg_lo = seg * CK_SEG;
+    const size_t s_lo = seg_lo + (size_t)tid * CK_SLICE;
+    const size_t v_lo = s_lo > lo ? s_lo : lo;                              // valid start
+    const size_t v_hi = (s_lo + CK_SLICE) < hi ? (s_lo + CK_SLICE) : hi;    // valid end
+    uint32_t c = 0, s1 = 0, s2 = 0, len = 0;
+    if (v_lo == s_lo && v_hi == s_lo + CK_SLICE) {
+      len = CK_SLICE;
+      const uint4 *p = reinterpret_cast<const uint4 *>(frame + s_lo);
+#pragma unroll 1
+      for (int line = 0; line < CK_SLICE / 128; ++line) {
+        uint4 v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = ld_stream(p + line * 8 + k);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          if (DO_CRC) {
+            c = crc_step8(c, v[k].x, v[k].y, T, lane32);
+            c = crc_step8(c, v[k].z, v[k].w, T, lane32);
+          }
+          if (DO_ADLER) adler16(s1, s2, v[k]);
+        }
+      }
+    } else if (v_lo < v_hi) {
+      // ragged slice (first/last segment only): byte at a time
+      len = (uint32_t)(v_hi - v_lo);
+      for (size_t i = v_lo; i < v_hi; ++i) {
+        uint32_t b = frame[i];
+        if (DO_CRC) c = crc_byte(c, b);
+        if (DO_ADLER) {
+          s1 += b;
+          s2 += s1;
+        }
+      }
+    }
+    // ---- merge slices inside the segment ----
+    if (DO_CRC) {
+      red_c[tid] = c;
+      red_l[tid] = len;
+    }
+    uint64_t a1 = s1, a2 = 0;
+    if (DO_ADLER) {
+      // bytes after this slice within the segment's valid range
+      const size_t seg_v_hi = (seg_lo + CK_SEG) < hi ? (seg_lo + CK_SEG) : hi;
+      const size_t after = (v_hi >= v_lo && seg_v_hi > v_hi) ? seg_v_hi - (v_hi > v_lo ? v_hi : v_lo) : 0;
+      a2 = (uint64_t)s2 + (uint64_t)s1 * (len ? after : 0);
+      for (int off = 32; off > 0; off >>= 1) {
+        a1 += __shfl_down(a1, off, 64);
+        a2 += __shfl_down(a2, off, 64);
+      }
+      if ((tid & 63) == 0) {
+        red_a[tid >> 6][0] = a1;
+        red_a[tid >> 6][1] = a2;
+      }
+    }
+    __syncthreads();
+    if (DO_CRC) {
+#pragma unroll 1
+      for (int step = 1; step < CK_THREADS; step <<= 1) {
+        if ((tid & (2 * step - 1)) == 0) {
+          uint32_t rl = red_l[tid + step];
+          uint32_t rc = red_c[tid + step];
+          uint32_t lc = red_c[tid];
+          if (rl) lc = multmodp(x2nmodp(x2n, rl, 3), lc);
+          red_c[tid] = lc ^ rc;
+          red_l[tid] += rl;
+        }
+        __syncthreads();
+      }
+    }
+    if (tid == 0) {
+      SegResult r;
+      r.crc = DO_CRC ? red_c[0] : 0;
+      uint64_t t1 = 0, t2 = 0;
+      if (DO_ADLER) {
+        for (int w = 0; w < CK_THREADS / 64; ++w) {
+          t1 += red_a[w][0];
+          t2 += red_a[w][1];
+        }
+      }
+      r.s1 = (uint32_t)(t1 % 65521u);
+      r.s2 = (uint32_t)(t2 % 65521u);
+      size_t sv_lo = seg_lo > lo ? seg_lo : lo;
+      size_t sv_hi = (seg_lo + CK_SEG) < hi ? (seg_lo + CK_SEG) : hi;
+      r.len = sv_hi > sv_lo ? (uint32_t)(sv_hi - sv_lo) : 0;
+      out[seg] = r;
+    }
+    __syncthreads();
+  }
+}
+
+// Merge per-segment results in order and apply the callers' initial values.
+__global__ __launch_bounds__(256) void checksum_finish(const SegResult *__restrict__ segs, size_t nseg, uint64_t n,
+                                                       const uint32_t *__restrict__ x2n_g, uint32_t crc_in,
+                                                       uint32_t adler_in, uint32_t *__restrict__ result) {
+  __shared__ uint32_t x2n[32];
+  __shared__ uint32_t rc[256];
+  __shared__ uint64_t rl[256];
+  __shared__ uint64_t r1[256], r2[256];
+  const int tid = threadIdx.x;
+  if (tid < 32) x2n[tid] = x2n_g[tid];
+  __syncthreads();
+  // thread t folds a contiguous run of segments
+  const size_t per = (nseg + 255) / 256;
+  const size_t b = (size_t)tid * per, e = (b + per) < nseg ? (b + per) : nseg;
+  uint32_t c = 0;
+  uint64_t l = 0, s1 = 0, s2 = 0;
+  for (size_t i = b; i < e; ++i) {
+    SegResult r = segs[i];
+    if (r.len) c = multmodp(x2nmodp(x2n, r.len, 3), c);
+    c ^= r.crc;
+    s2 = (s2 + (uint64_t)r.len % 65521u * s1 + r.s2) % 65521u;
+    s1 = (s1 + r.s1) % 65521u;
+    l += r.len;
+  }
+  rc[tid] = c;
+  rl[tid] = l;
+  r1[tid] = s1;
+  r2[tid] = s2;
+  __syncthreads();
+  for (int step = 1; step < 256; step <<= 1) {
+    if ((tid & (2 * step - 1)) == 0) {
+      uint64_t L = rl[tid + step];
+      if (L) rc[tid] = multmodp(x2nmodp(x2n, L, 3), rc[tid]);
+      rc[tid] ^= rc[tid + step];
+      r2[tid] = (r2[tid] + L % 65521u * r1[tid] + r2[tid + step]) % 65521u;
+      r1[tid] = (r1[tid] + r1[tid + step]) % 65521u;
+      rl[tid] += L;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    // CRC32.update: ~(shift(~crc, n) ^ raw)
+    uint32_t pre = ~crc_in;
+    pre = multmodp(x2nmodp(x2n, n, 3), pre);
+    result[0] = ~(pre ^ rc[0]);
+    // Adler32.update: s1 = adler & 0xFFFF, s2 = (adler >> 16) & 0xFFFF (need not be reduced)
+    uint64_t a = adler_in & 0xFFFFu, bb = (adler_in >> 16) & 0xFFFFu;
+    uint64_t f1 = (a + r1[0]) % 65521u;
+    uint64_t f2 = (bb + (n % 65521u) * (a % 65521u) + r2[0]) % 65521u;
+    result[1] = (uint32_t)((f2 << 16) | f1);
+  }
+}
+
+}  // namespace
+
+void crc_host_tables(uint32_t byte_table[256], uint32_t nib[256], uint32_t x2n[32]) {
+  for (uint32_t i = 0; i < 256; ++i) {
+    uint32_t c = i;
+    for (int j = 0; j < 8; ++j) c = (c & 1) ? (ZT_CRC_POLY ^ (c >> 1)) : (c >> 1);
+    byte_table[i] = c;
+  }
+  // nib[pos*16 + v]: raw CRC (init 0) of an 8-byte block whose only non-zero
+  // nibble is v at nibble position pos (byte pos/2, high half when pos is odd)
+  for (int pos = 0; pos < 16; ++pos) {
+    for (uint32_t v = 0; v < 16; ++v) {
+      uint8_t blk[8] = {0};
+      blk[pos >> 1] = (uint8_t)(v << (4 * (pos & 1)));
+      uint32_t c = 0;
+      for (int k = 0; k < 8; ++k) c = (c >> 8) ^ byte_table[(c ^ blk[k]) & 0xFF];
+      nib[pos * 16 + v] = c;
+    }
+  }
+  x2n[0] = 1u << 30;  // x^1
+  for (int k = 1; k < 32; ++k) x2n[k] = multmodp(x2n[k - 1], x2n[k - 1]);
+}
+
+int checksums_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, bool do_crc, bool do_adler, uint32_t crc_in,
+                  uint32_t adler_in, uint32_t *d_result, hipStream_t s) {
+  const uintptr_t addr = reinterpret_cast<uintptr_t>(d_in);
+  const uint8_t *frame = reinterpret_cast<const uint8_t *>(addr & ~uintptr_t(15));
+  const size_t lo = addr & 15, hi = lo + n;
+  const size_t nseg = n ? (hi + CK_SEG - 1) / CK_SEG : 1;
+  void *segbuf;
+  ZT_TRY(scratch(c, 3, nseg * sizeof(SegResult), &segbuf));
+  SegResult *segs = static_cast<SegResult *>(segbuf);
+  const int grid = (int)(nseg < (size_t)c->num_cu * 8 ? nseg : (size_t)c->num_cu * 8);
+  if (do_crc && do_adler)
+    checksum_segments<true, true><<<grid, CK_THREADS, 0, s>>>(frame, lo, hi, nseg, c->d_crc_nib, c->d_crc_x2n, segs);
+  else if (do_crc)
+    checksum_segments<true, false><<<grid, CK_THREADS, 0, s>>>(frame, lo, hi, nseg, c->d_crc_nib, c->d_crc_x2n, segs);
+  else
+    checksum_segments<false, true><<<grid, CK_THREADS, 0, s>>>(frame, lo, hi, nseg, c->d_crc_nib, c->d_crc_x2n, segs);
+  ZT_HIP(hipGetLastError());
+  checksum_finish<<<1, 256, 0, s>>>(segs, nseg, n, c->d_crc_x2n, crc_in, adler_in, d_result);
+  ZT_HIP(hipGetLastError());
+  return ZT_OK;
+}
+
+}  // namespace zt

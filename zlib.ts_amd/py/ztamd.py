@@ -1,0 +1,244 @@
+"""ztamd -- ctypes binding of libzt.so (include/zt.h) for tests and bench.py.
+
+This is plumbing over the C-ABI, not a second implementation: every call runs
+on the GPU through libzt.so.  Importing fails loudly when the library has not
+been built (``make -C zlib.ts_amd`` / ``__graft_entry__.build()``).
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIBPATH = os.path.join(os.path.dirname(HERE), "libzt.so")
+
+ZT_OK = 0
+ERRORS = {
+    -1: "ZT_E_INVALID_COMPRESSION_TYPE", -2: "ZT_E_INVALID_INDEX", -10: "ZT_E_INPUT_BROKEN",
+    -11: "ZT_E_INVALID_CODE_LENGTH", -12: "ZT_E_UNKNOWN_BTYPE", -13: "ZT_E_STORED_LEN", -14: "ZT_E_STORED_NLEN",
+    -15: "ZT_E_INVALID_DISTANCE", -16: "ZT_E_INVALID_SYMBOL", -17: "ZT_E_BAD_TREE", -100: "ZT_E_NO_DEVICE",
+    -101: "ZT_E_HIP", -102: "ZT_E_NOMEM", -103: "ZT_E_ARG",
+}
+
+
+class ZtError(Exception):
+    def __init__(self, code, msg):
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}")
+        self.code = code
+        self.msg = msg
+
+
+class DeflateOpts(ctypes.Structure):
+    _fields_ = [("compression_type", ctypes.c_int), ("lazy", ctypes.c_int), ("level", ctypes.c_int)]
+
+
+class InflateOpts(ctypes.Structure):
+    _fields_ = [("buffer_type", ctypes.c_int), ("buffer_size", ctypes.c_size_t), ("ref_strict", ctypes.c_int)]
+
+
+def _load():
+    # torch (when present) ships its own libamdhip64.so.7; loading it first makes
+    # libzt.so bind to that same runtime (same SONAME) instead of starting a
+    # second HIP runtime in the process, which would leave torch without a GPU.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    if not os.path.exists(LIBPATH):
+        raise ImportError(f"libzt.so not built at {LIBPATH}; run make -C zlib.ts_amd")
+    lib = ctypes.CDLL(LIBPATH)
+    sz, vp, u32 = ctypes.c_size_t, ctypes.c_void_p, ctypes.c_uint32
+    u8pp = ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8))
+    P = ctypes.POINTER
+    sig = {
+        "zt_device_count": ([], ctypes.c_int),
+        "zt_set_device": ([ctypes.c_int], ctypes.c_int),
+        "zt_last_error_message": ([], ctypes.c_char_p),
+        "zt_version": ([], ctypes.c_char_p),
+        "zt_free": ([vp], None),
+        "zt_crc32_update": ([u32, vp, sz, P(u32)], ctypes.c_int),
+        "zt_adler32_update": ([u32, vp, sz, P(u32)], ctypes.c_int),
+        "zt_checksums": ([vp, sz, u32, u32, P(u32), P(u32)], ctypes.c_int),
+        "zt_deflate_raw": ([vp, sz, P(DeflateOpts), u8pp, P(sz)], ctypes.c_int),
+        "zt_inflate_raw": ([vp, sz, sz, P(InflateOpts), u8pp, P(sz), P(sz)], ctypes.c_int),
+        "zt_inflate_raw_batch": ([P(vp), P(sz), sz, P(InflateOpts), u8pp, P(sz), P(sz), P(ctypes.c_int)],
+                                 ctypes.c_int),
+        "zt_deflate_raw_batch": ([P(vp), P(sz), sz, P(DeflateOpts), u8pp, P(sz), P(ctypes.c_int)], ctypes.c_int),
+        "zt_dev_checksums": ([vp, sz, u32, u32, P(u32), P(u32), vp], ctypes.c_int),
+        "zt_deflate_plan_create": ([sz, P(DeflateOpts), P(vp)], ctypes.c_int),
+        "zt_deflate_plan_destroy": ([vp], None),
+        "zt_deflate_bound": ([sz], sz),
+        "zt_deflate_dev": ([vp, vp, sz, sz, ctypes.c_int, vp, P(sz), vp], ctypes.c_int),
+        "zt_inflate_plan_create": ([sz, sz, P(vp)], ctypes.c_int),
+        "zt_inflate_plan_destroy": ([vp], None),
+        "zt_inflate_dev": ([vp, vp, sz, vp, sz, P(sz), P(sz), vp], ctypes.c_int),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(lib, name, None)
+        if f is None:  # reported by tests/test_abi.py
+            continue
+        f.argtypes = args
+        f.restype = res
+    return lib
+
+
+lib = _load()
+
+# every symbol include/zt.h declares (checked by tests/test_abi.py)
+SYMBOLS = [
+    "zt_device_count", "zt_set_device", "zt_last_error_message", "zt_version", "zt_free", "zt_crc32_update",
+    "zt_adler32_update", "zt_checksums", "zt_deflate_raw", "zt_inflate_raw", "zt_inflate_raw_batch",
+    "zt_deflate_raw_batch", "zt_dev_checksums", "zt_deflate_plan_create", "zt_deflate_plan_destroy",
+    "zt_deflate_bound", "zt_deflate_dev", "zt_inflate_plan_create", "zt_inflate_plan_destroy", "zt_inflate_dev",
+]
+
+
+def _check(rc):
+    if rc != ZT_OK:
+        raise ZtError(rc, lib.zt_last_error_message().decode(errors="replace"))
+
+
+def _cbuf(data):
+    data = bytes(data)
+    return ctypes.create_string_buffer(data, len(data) or 1), len(data)
+
+
+def device_count():
+    return lib.zt_device_count()
+
+
+def set_device(d):
+    _check(lib.zt_set_device(d))
+
+
+def crc32(data, crc=0):
+    b, n = _cbuf(data)
+    out = ctypes.c_uint32()
+    _check(lib.zt_crc32_update(crc, b, n, ctypes.byref(out)))
+    return out.value
+
+
+def adler32(data, adler=1):
+    b, n = _cbuf(data)
+    out = ctypes.c_uint32()
+    _check(lib.zt_adler32_update(adler, b, n, ctypes.byref(out)))
+    return out.value
+
+
+def checksums(data, crc=0, adler=1):
+    b, n = _cbuf(data)
+    c, a = ctypes.c_uint32(), ctypes.c_uint32()
+    _check(lib.zt_checksums(b, n, crc, adler, ctypes.byref(c), ctypes.byref(a)))
+    return c.value, a.value
+
+
+def deflate_raw(data, compression_type=2, lazy=0, level=-1):
+    b, n = _cbuf(data)
+    opts = DeflateOpts(compression_type, lazy, level)
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    olen = ctypes.c_size_t()
+    _check(lib.zt_deflate_raw(b, n, ctypes.byref(opts), ctypes.byref(out), ctypes.byref(olen)))
+    res = ctypes.string_at(out, olen.value)
+    lib.zt_free(out)
+    return res
+
+
+def inflate_raw(data, index=0, ref_strict=False, buffer_type=1, buffer_size=0x8000):
+    """Returns (output bytes, end ip)."""
+    b, n = _cbuf(data)
+    opts = InflateOpts(buffer_type, buffer_size, 1 if ref_strict else 0)
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    olen = ctypes.c_size_t()
+    ip = ctypes.c_size_t()
+    _check(lib.zt_inflate_raw(b, n, index, ctypes.byref(opts), ctypes.byref(out), ctypes.byref(olen),
+                              ctypes.byref(ip)))
+    res = ctypes.string_at(out, olen.value)
+    lib.zt_free(out)
+    return res, ip.value
+
+
+def inflate_raw_batch(streams, ref_strict=False):
+    """Returns a list of (status, output bytes, end ip)."""
+    k = len(streams)
+    bufs = [_cbuf(s) for s in streams]
+    ptrs = (ctypes.c_void_p * k)(*[ctypes.addressof(b) for b, _ in bufs])
+    lens = (ctypes.c_size_t * k)(*[n for _, n in bufs])
+    outs = (ctypes.POINTER(ctypes.c_uint8) * k)()
+    olens = (ctypes.c_size_t * k)()
+    ips = (ctypes.c_size_t * k)()
+    st = (ctypes.c_int * k)()
+    opts = InflateOpts(1, 0x8000, 1 if ref_strict else 0)
+    rc = lib.zt_inflate_raw_batch(ptrs, lens, k, ctypes.byref(opts), outs, olens, ips, st)
+    if rc != ZT_OK and all(s == 0 for s in st):
+        _check(rc)
+    res = []
+    for i in range(k):
+        data = ctypes.string_at(outs[i], olens[i]) if st[i] == 0 and outs[i] else b""
+        if outs[i]:
+            lib.zt_free(outs[i])
+        res.append((st[i], data, ips[i]))
+    return res
+
+
+def deflate_raw_batch(items, compression_type=2, level=-1):
+    k = len(items)
+    bufs = [_cbuf(s) for s in items]
+    ptrs = (ctypes.c_void_p * k)(*[ctypes.addressof(b) for b, _ in bufs])
+    lens = (ctypes.c_size_t * k)(*[n for _, n in bufs])
+    outs = (ctypes.POINTER(ctypes.c_uint8) * k)()
+    olens = (ctypes.c_size_t * k)()
+    st = (ctypes.c_int * k)()
+    opts = DeflateOpts(compression_type, 0, level)
+    rc = lib.zt_deflate_raw_batch(ptrs, lens, k, ctypes.byref(opts), outs, olens, st)
+    _check(rc)
+    res = []
+    for i in range(k):
+        res.append(ctypes.string_at(outs[i], olens[i]))
+        lib.zt_free(outs[i])
+    return res
+
+
+# ---- device-resident helpers (torch tensors as HBM buffers) -----------------------
+def dev_checksums(ptr, n, crc=0, adler=1, stream=None):
+    c, a = ctypes.c_uint32(), ctypes.c_uint32()
+    _check(lib.zt_dev_checksums(ptr, n, crc, adler, ctypes.byref(c), ctypes.byref(a), stream))
+    return c.value, a.value
+
+
+class DeflatePlan:
+    def __init__(self, max_n, level=-1, compression_type=2):
+        self.h = ctypes.c_void_p()
+        opts = DeflateOpts(compression_type, 0, level)
+        _check(lib.zt_deflate_plan_create(max_n, ctypes.byref(opts), ctypes.byref(self.h)))
+
+    def run(self, d_in, n, d_out, halo=0, final=1, stream=None):
+        olen = ctypes.c_size_t()
+        _check(lib.zt_deflate_dev(self.h, d_in, n, halo, final, d_out, ctypes.byref(olen), stream))
+        return olen.value
+
+    def close(self):
+        if self.h:
+            lib.zt_deflate_plan_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+    __del__ = close
+
+
+class InflatePlan:
+    def __init__(self, max_in, max_out):
+        self.h = ctypes.c_void_p()
+        _check(lib.zt_inflate_plan_create(max_in, max_out, ctypes.byref(self.h)))
+
+    def run(self, d_in, n, d_out, out_cap, stream=None):
+        olen, ip = ctypes.c_size_t(), ctypes.c_size_t()
+        _check(lib.zt_inflate_dev(self.h, d_in, n, d_out, out_cap, ctypes.byref(olen), ctypes.byref(ip), stream))
+        return olen.value, ip.value
+
+    def close(self):
+        if self.h:
+            lib.zt_inflate_plan_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+    __del__ = close
+
+
+def deflate_bound(n):
+    return lib.zt_deflate_bound(n)
