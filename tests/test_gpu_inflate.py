@@ -1,0 +1,168 @@
+"""RawInflate on the GPU (libzt.so) vs the oracle, the reference-generated
+vectors and independent zlib streams."""
+import random
+import zlib
+
+import pytest
+
+from golden_util import blob_bytes, blob_matches, load, make_input
+from zt_oracle import OracleError
+
+pytestmark = pytest.mark.gpu
+
+INF = load("inflate.json")
+DF = load("deflate.json")
+
+
+@pytest.fixture(scope="module")
+def zt():
+    import ztamd
+
+    assert ztamd.device_count() > 0, "no GPU visible"
+    return ztamd
+
+
+def _rid(r):
+    return f"{str(r['origin'])[:60]}|{r['opts']}"
+
+
+@pytest.mark.parametrize("rec", INF["records"], ids=_rid)
+def test_golden_strict(zt, rec):
+    """ref_strict=True reproduces the reference exactly: output, .ip and the
+    error text (src/RawInflate.ts messages), including its over-strict EOF
+    rejections of valid streams."""
+    import ztamd
+
+    s = blob_bytes(rec["stream"])
+    index = rec["opts"].get("index", 0)
+    if "error" in rec:
+        with pytest.raises(ztamd.ZtError) as ei:
+            zt.inflate_raw(s, index=index, ref_strict=True)
+        assert ei.value.msg == rec["error"]
+        return
+    out, ip = zt.inflate_raw(s, index=index, ref_strict=True)
+    assert ip == rec["ip"]
+    if rec["opts"].get("bufferType") == 0 and len(out) > 32768:
+        # documented divergence: the reference's BLOCK buffer mode corrupts
+        # outputs > 32 KiB (src/RawInflate.ts:530); the engine decodes correctly
+        assert out == zlib.decompress(s[index:], -15)
+        return
+    assert blob_matches(rec["out"], out)
+
+
+@pytest.mark.parametrize("rec", INF["records"], ids=_rid)
+def test_golden_rfc(zt, rec):
+    """Default mode decodes every valid stream, matching zlib (and the
+    reference wherever the reference succeeds)."""
+    import ztamd
+
+    s = blob_bytes(rec["stream"])
+    index = rec["opts"].get("index", 0)
+    try:
+        ref = zlib.decompressobj(-15)
+        want = ref.decompress(s[index:]) + ref.flush()
+        valid = ref.eof
+    except zlib.error:
+        valid = False
+    if not valid:
+        with pytest.raises(ztamd.ZtError):
+            zt.inflate_raw(s, index=index)
+        return
+    out, ip = zt.inflate_raw(s, index=index)
+    assert out == want
+    assert ip == len(s) - len(ref.unused_data)
+
+
+def test_reference_deflate_outputs(zt, oracle):
+    """Every stream the reference's RawDeflate produced decodes to its input
+    (lazy>0 streams excepted where the reference's own bug corrupted them)."""
+    n = 0
+    for rec in DF["records"]:
+        if "hex" not in rec.get("out", {}) or rec["opts"].get("compressionType") == 0:
+            continue
+        if rec.get("zlib_ok") is False:
+            # the reference emitted an invalid stream (lazy>0 duplication bug,
+            # src/LZ77.ts:228-239, or the dropped EOB of an empty FIXED block)
+            continue
+        if "outputBuffer" in rec["opts"]:
+            continue
+        d = make_input(rec["input"], oracle)
+        s = bytes.fromhex(rec["out"]["hex"])
+        out, ip = zt.inflate_raw(s)
+        assert out == d
+        assert ip == len(s)
+        n += 1
+    assert n > 50
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_vs_oracle_random(zt, oracle, seed):
+    rng = random.Random(seed)
+    for _ in range(8):
+        kind = rng.choice(["xorshift32", "wordsalad", "structured"])
+        n = rng.choice([0, 1, 5, 100, 4095, 4096, 4097, 40000, 70000, 300000])
+        d = oracle.gen(kind, rng.randrange(1, 1 << 30), n)
+        level = rng.choice([0, 1, 3, 6, 9])
+        strategy = rng.choice([zlib.Z_DEFAULT_STRATEGY, zlib.Z_FILTERED, zlib.Z_HUFFMAN_ONLY, zlib.Z_RLE,
+                               zlib.Z_FIXED])
+        c = zlib.compressobj(level, zlib.DEFLATED, -15, 9, strategy)
+        s = c.compress(d) + c.flush()
+        out, ip = zt.inflate_raw(s)
+        assert out == d and ip == len(s)
+        try:
+            ro, rip = oracle.raw_inflate(s)
+            out2, ip2 = zt.inflate_raw(s, ref_strict=True)
+            assert (out2, ip2) == (ro, rip)
+        except OracleError as e:
+            import ztamd
+
+            with pytest.raises(ztamd.ZtError) as ei:
+                zt.inflate_raw(s, ref_strict=True)
+            assert ei.value.msg == e.msg
+
+
+def test_large_and_highly_compressible(zt, oracle):
+    # output far larger than the first capacity guess (retry path)
+    d = b"\0" * (50 << 20)
+    s = zlib.compress(d, 9)[2:-4]
+    out, ip = zt.inflate_raw(s)
+    assert out == d and ip == len(s)
+    d = oracle.gen("wordsalad", 9, 20 << 20)
+    s = zlib.compress(d, 6)[2:-4]
+    assert zt.inflate_raw(s)[0] == d
+
+
+def test_sync_flush_streams(zt, oracle):
+    d = oracle.gen("wordsalad", 77, 1 << 20)
+    c = zlib.compressobj(6, zlib.DEFLATED, -15)
+    parts = []
+    for o in range(0, len(d), 32768):
+        parts.append(c.compress(d[o:o + 32768]) + c.flush(zlib.Z_SYNC_FLUSH))
+    parts.append(c.flush())
+    s = b"".join(parts)
+    assert zt.inflate_raw(s) == (d, len(s))
+
+
+def test_batch(zt, oracle):
+    rng = random.Random(5)
+    items = []
+    for i in range(300):
+        n = rng.choice([0, 10, 1000, 65536, 200000])
+        d = oracle.gen(["xorshift32", "wordsalad", "structured"][i % 3], 100 + i, n)
+        items.append((d, zlib.compress(d, rng.choice([1, 6, 9]))[2:-4]))
+    bad = b"\x07\x00"
+    res = zt.inflate_raw_batch([s for _, s in items] + [bad])
+    for (d, s), (st, out, ip) in zip(items, res):
+        assert st == 0 and out == d and ip == len(s)
+    assert res[-1][0] == -12  # unknown BTYPE: 3
+
+
+def test_errors(zt):
+    import ztamd
+
+    cases = {b"\x07": "unknown BTYPE: 3", b"": "input buffer is broken", b"\x00": "invalid uncompressed block header: LEN",
+             b"\x01\x05\x00\xfa\xff": "input buffer is broken"}
+    for s, msg in cases.items():
+        with pytest.raises(ztamd.ZtError) as ei:
+            zt.inflate_raw(s)
+        assert ei.value.msg == msg

@@ -83,4 +83,27 @@ void crc_host_tables(uint32_t byte_table[256], uint32_t nib[256], uint32_t x2n[3
 int checksums_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, bool do_crc, bool do_adler, uint32_t crc_in,
                   uint32_t adler_in, uint32_t *d_result /* [2] */, hipStream_t s);
 
+// ---- inflate jobs (one stream per wavefront) -----------------------------------
+struct InfJob {
+  const uint8_t *in;  // whole input array (RawInflate's `input`)
+  uint64_t n;         // its length
+  uint64_t start;     // RawInflate `index`
+  uint8_t *out;       // output buffer (device)
+  uint64_t cap;       // output capacity; decoding continues past it, counting only
+  int32_t strict;     // stop with 'input buffer is broken' where the reference's EOF test throws
+  int32_t pad;
+};
+
+struct InfResult {
+  uint64_t out_len;     // bytes produced (may exceed cap)
+  uint64_t end_ip;      // reference .ip after decompress
+  int32_t status;
+  int32_t detail;       // code length / BTYPE for the message
+  int32_t strict_fail;  // reference's readBits EOF check would throw
+  int32_t pad;
+};
+
+int inflate_jobs_dev(const InfJob *d_jobs, InfResult *d_res, int count, hipStream_t s);
+int inflate_error(int status, int detail);
+
 }  // namespace zt
