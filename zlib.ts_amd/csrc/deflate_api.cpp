@@ -1,0 +1,186 @@
+// deflate_api.cpp -- host side of the deflate entry points and the
+// device-resident plans (include/zt.h).
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "zt_internal.h"
+
+namespace zt {
+
+size_t deflate_bound_bytes(size_t n);
+size_t deflate_scratch_bytes(const DeviceCtx *c, size_t n);
+int deflate_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t halo, int final_, int ctype, int level,
+                    uint8_t *d_out, size_t *out_len, void *scratch_base, size_t scratch_size, hipStream_t s);
+
+static int resolve(const zt_deflate_opts *o, int *ctype, int *level) {
+  int ct = o ? o->compression_type : 2;
+  int lv = o ? o->level : -1;
+  if (ct < 0 || ct > 2) return set_error(ZT_E_INVALID_COMPRESSION_TYPE, "invalid compression type");
+  if (lv < 0 || lv > 9) lv = 6;
+  if (lv == 0) ct = 0;
+  // the reference's `lazy` option asks for deferred matching: use the lazy parse
+  if (o && o->lazy > 0 && lv < 4) lv = 4;
+  *ctype = ct;
+  *level = lv;
+  return ZT_OK;
+}
+
+static size_t out_bound(int ctype, size_t n) {
+  if (ctype == 0) return n + 5 * ((n + 65534) / 65535) + 16;
+  return deflate_bound_bytes(n) + (ctype == 1 ? n / 8 + 64 : 0);
+}
+
+}  // namespace zt
+
+using namespace zt;
+
+struct zt_deflate_plan {
+  int device;
+  int ctype, level;
+  size_t max_n;
+  void *scratch;
+  size_t scratch_size;
+};
+
+struct zt_inflate_plan {
+  int device;
+  size_t max_in, max_out;
+  void *jobs;
+};
+
+namespace zt {
+extern uint32_t *g_deflate_debug;
+}
+
+extern "C" {
+
+// Test hook (not part of include/zt.h): dump the first sub-chunk's per-position
+// match results and parse masks into a device buffer of >= 17000 words.
+int zt_debug_set_deflate_dump(void *d_buf) {
+  g_deflate_debug = (uint32_t *)d_buf;
+  return ZT_OK;
+}
+
+size_t zt_deflate_bound(size_t n) { return out_bound(1, n) + out_bound(0, n); }
+
+int zt_deflate_plan_create(size_t max_n, const zt_deflate_opts *opts, zt_deflate_plan **plan) {
+  if (!plan) return set_error(ZT_E_ARG, "null plan");
+  DeviceCtx *c;
+  ZT_TRY(get_ctx(&c));
+  int ct, lv;
+  ZT_TRY(resolve(opts, &ct, &lv));
+  zt_deflate_plan *p = new zt_deflate_plan();
+  p->device = c->device;
+  p->ctype = ct;
+  p->level = lv;
+  p->max_n = max_n;
+  p->scratch_size = deflate_scratch_bytes(c, max_n);
+  hipError_t e = hipMalloc(&p->scratch, p->scratch_size);
+  if (e != hipSuccess) {
+    delete p;
+    return hip_fail(e, "hipMalloc(deflate scratch)");
+  }
+  *plan = p;
+  return ZT_OK;
+}
+
+void zt_deflate_plan_destroy(zt_deflate_plan *plan) {
+  if (!plan) return;
+  if (plan->scratch) (void)hipFree(plan->scratch);
+  delete plan;
+}
+
+int zt_deflate_dev(zt_deflate_plan *plan, const void *d_in, size_t n, size_t halo, int final_, void *d_out,
+                   size_t *out_len, void *stream) {
+  if (!plan || !out_len) return set_error(ZT_E_ARG, "null argument");
+  if (n > plan->max_n) return set_error(ZT_E_ARG, "input larger than the plan");
+  DeviceCtx *c;
+  ZT_TRY(get_ctx(&c));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  if (halo > 32768) halo = 32768;
+  return deflate_dev_run(c, (const uint8_t *)d_in, n, halo, final_, plan->ctype, plan->level, (uint8_t *)d_out,
+                         out_len, plan->scratch, plan->scratch_size, s);
+}
+
+int zt_deflate_raw(const uint8_t *in, size_t n, const zt_deflate_opts *opts, uint8_t **out, size_t *out_len) {
+  if (!out || !out_len) return set_error(ZT_E_ARG, "null output");
+  if (n && !in) return set_error(ZT_E_ARG, "null input");
+  DeviceCtx *c;
+  ZT_TRY(get_ctx(&c));
+  int ct, lv;
+  ZT_TRY(resolve(opts, &ct, &lv));
+  const size_t ob = out_bound(ct, n);
+  void *d_in, *d_out, *d_scr;
+  ZT_TRY(scratch(c, 0, n + 64, &d_in));
+  ZT_TRY(scratch(c, 1, ob, &d_out));
+  const size_t ss = deflate_scratch_bytes(c, n);
+  ZT_TRY(scratch(c, 3, ss, &d_scr));
+  if (n) ZT_HIP(hipMemcpyAsync(d_in, in, n, hipMemcpyHostToDevice, c->stream));
+  size_t len = 0;
+  ZT_TRY(deflate_dev_run(c, (const uint8_t *)d_in, n, 0, 1, ct, lv, (uint8_t *)d_out, &len, d_scr, ss, c->stream));
+  uint8_t *h = (uint8_t *)malloc(len ? len : 1);
+  if (!h) return set_error(ZT_E_NOMEM, "host allocation failed");
+  ZT_HIP(hipMemcpyAsync(h, d_out, len, hipMemcpyDeviceToHost, c->stream));
+  ZT_HIP(hipStreamSynchronize(c->stream));
+  *out = h;
+  *out_len = len;
+  return ZT_OK;
+}
+
+int zt_deflate_raw_batch(const uint8_t *const *in, const size_t *n, size_t count, const zt_deflate_opts *opts,
+                         uint8_t **out, size_t *out_len, int *status) {
+  if (!in || !n || !out || !out_len || !status) return set_error(ZT_E_ARG, "null argument");
+  int first = ZT_OK;
+  for (size_t i = 0; i < count; ++i) {
+    status[i] = zt_deflate_raw(in[i], n[i], opts, &out[i], &out_len[i]);
+    if (status[i] && first == ZT_OK) first = status[i];
+  }
+  return first;
+}
+
+int zt_inflate_plan_create(size_t max_in, size_t max_out, zt_inflate_plan **plan) {
+  if (!plan) return set_error(ZT_E_ARG, "null plan");
+  DeviceCtx *c;
+  ZT_TRY(get_ctx(&c));
+  zt_inflate_plan *p = new zt_inflate_plan();
+  p->device = c->device;
+  p->max_in = max_in;
+  p->max_out = max_out;
+  hipError_t e = hipMalloc(&p->jobs, 4096);
+  if (e != hipSuccess) {
+    delete p;
+    return hip_fail(e, "hipMalloc(inflate plan)");
+  }
+  *plan = p;
+  return ZT_OK;
+}
+
+void zt_inflate_plan_destroy(zt_inflate_plan *plan) {
+  if (!plan) return;
+  if (plan->jobs) (void)hipFree(plan->jobs);
+  delete plan;
+}
+
+int zt_inflate_dev(zt_inflate_plan *plan, const void *d_in, size_t n, void *d_out, size_t out_cap, size_t *out_len,
+                   size_t *end_ip, void *stream) {
+  if (!plan || !out_len) return set_error(ZT_E_ARG, "null argument");
+  DeviceCtx *c;
+  ZT_TRY(get_ctx(&c));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  InfJob job{(const uint8_t *)d_in, n, 0, (uint8_t *)d_out, out_cap, 0, 0};
+  InfJob *dj = (InfJob *)plan->jobs;
+  InfResult *dr = (InfResult *)((uint8_t *)plan->jobs + 256);
+  ZT_HIP(hipMemcpyAsync(dj, &job, sizeof job, hipMemcpyHostToDevice, s));
+  ZT_TRY(inflate_jobs_dev(dj, dr, 1, s));
+  InfResult r;
+  ZT_HIP(hipMemcpyAsync(&r, dr, sizeof r, hipMemcpyDeviceToHost, s));
+  ZT_HIP(hipStreamSynchronize(s));
+  if (r.status) return inflate_error(r.status, r.detail);
+  if (r.out_len > out_cap) return set_error(ZT_E_ARG, "output capacity too small");
+  *out_len = r.out_len;
+  if (end_ip) *end_ip = r.end_ip;
+  return ZT_OK;
+}
+
+}  // extern "C"
