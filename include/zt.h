@@ -122,10 +122,27 @@ typedef struct zt_inflate_plan zt_inflate_plan;
 int zt_inflate_plan_create(size_t max_in, size_t max_out, zt_inflate_plan **plan);
 void zt_inflate_plan_destroy(zt_inflate_plan *plan);
 /* Inflate the raw stream d_in[0..n) into d_out (capacity out_cap).  Streams
- * with byte-aligned sync points (empty stored blocks, as zt_deflate_dev and
- * zlib Z_SYNC_FLUSH emit) are decoded chunk-parallel. */
+ * carrying restart points (two empty stored blocks, which zt_deflate_dev
+ * writes every 1 MiB of input) are decoded segment-parallel; others by one
+ * wavefront.  Results are identical either way. */
 int zt_inflate_dev(zt_inflate_plan *plan, const void *d_in, size_t n, void *d_out, size_t out_cap,
                    size_t *out_len, size_t *end_ip, void *stream);
+
+/* ---- benchmark / test support (no reference counterpart) ---- */
+/* Synthetic corpus: 64 KiB piece i is generator `kind`
+ * (0 xorshift32, 1 wordsalad, 2 structured int32 deltas, 3 mixed per 4 MiB
+ * window) seeded with seed + i.  d_out must be 4-byte aligned. */
+int zt_synth_dev(int kind, uint32_t seed, void *d_out, size_t n, void *stream);
+/* Kernel-time accounting with HIP events on the launch stream: the deflate
+ * LZ77/Huffman kernel and the inflate decode kernel of the device paths. */
+typedef struct {
+  double deflate_ms;
+  uint64_t deflate_launches;
+  double inflate_ms;
+  uint64_t inflate_launches;
+} zt_kernel_times;
+int zt_timing_enable(int on); /* resets the counters */
+int zt_timing_read(zt_kernel_times *out);
 
 #ifdef __cplusplus
 }

@@ -94,3 +94,51 @@ def test_device_shards_concatenate(zt, oracle):
         parts.append(out[:n].cpu().numpy().tobytes())
     s = b"".join(parts)
     check_stream(oracle, zt, d, s)
+
+
+def test_segment_parallel_inflate(zt, oracle):
+    """Streams longer than one segment (1 MiB) carry restart markers; the
+    segment-parallel inflate must give exactly the one-wave result (host and
+    device-resident entry points)."""
+    import torch
+
+    d = b"".join(oracle.gen(k, 300 + i, (1 << 20) + 12345 * i)
+                 for i, k in enumerate(["wordsalad", "structured", "xorshift32", "wordsalad", "structured"]))
+    s = zt.deflate_raw(d)
+    assert s.count(b"\0\0\0\xff\xff\0\0\0\xff\xff") >= 4
+    assert zlib.decompress(s, -15) == d
+    out, ip = zt.inflate_raw(s)
+    assert out == d and ip == len(s)
+    strict, sip = zt.inflate_raw(s, ref_strict=True)  # one-wave path
+    assert strict == d and sip == ip
+    # device plan
+    di = torch.frombuffer(bytearray(s), dtype=torch.uint8).cuda()
+    do = torch.empty(len(d) + 100, dtype=torch.uint8, device="cuda")
+    p = zt.InflatePlan(len(s), len(d))
+    olen, eip = p.run(di.data_ptr(), len(s), do.data_ptr(), do.numel())
+    assert olen == len(d) and eip == len(s)
+    assert bytes(do[:olen].cpu().numpy()) == d
+    # index > 0: the stream starts inside a larger buffer
+    pre = b"hdr" * 7
+    out2, ip2 = zt.inflate_raw(pre + s, index=len(pre))
+    assert out2 == d and ip2 == len(pre) + len(s)
+
+
+def test_segment_false_candidates(zt, oracle):
+    """The restart pattern inside stored data (including exactly at a stored
+    block end) must not change the result."""
+    pat = b"\0\0\0\xff\xff\0\0\0\xff\xff"
+    chunk = bytearray(oracle.gen("xorshift32", 9, 65535))
+    chunk[-10:] = pat
+    chunk[1000:1010] = pat
+    d = bytes(chunk) * 8
+    s = zt.deflate_raw(d, compression_type=0)
+    assert zt.inflate_raw(s)[0] == d
+    # a Huffman stream followed by stored data holding the pattern
+    d2 = oracle.gen("wordsalad", 4, 1 << 19) + pat * 40000 + oracle.gen("xorshift32", 4, 1 << 19)
+    s2 = zt.deflate_raw(d2)
+    assert zt.inflate_raw(s2)[0] == d2
+    # truncated segmented stream: same error as the one-wave decode
+    s3 = zt.deflate_raw(oracle.gen("wordsalad", 5, 3 << 20))
+    with pytest.raises(zt.ZtError):
+        zt.inflate_raw(s3[: len(s3) // 2])

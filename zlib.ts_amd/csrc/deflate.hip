@@ -36,6 +36,8 @@ constexpr int DF_SLOT = DF_BLOCK + DF_BLOCK / 8 + 512;  // per-block slot: fits 
 constexpr int DF_HBITS = 13;
 constexpr int DF_THREADS = 1024;
 constexpr int DF_MAXDIST = 32768;
+// Independent segments of 1 MiB: restart points for segment-parallel inflate
+constexpr uint32_t kRestartBlocks = 32;
 
 struct DeflateParams {
   const uint8_t *base;  // stream bytes are base[halo .. halo + n)
@@ -43,6 +45,7 @@ struct DeflateParams {
   uint64_t end;         // halo + n
   uint32_t blocks_per_wg;
   uint32_t nblocks;
+  uint32_t restart;     // blocks per independent segment (multiple of blocks_per_wg)
   int final_;
   int max_chain;
   int nice_len;
@@ -792,7 +795,10 @@ __global__ __launch_bounds__(DF_THREADS) void deflate_kernel(DeflateParams P) {
   const uint32_t b1 = (b0 + P.blocks_per_wg) < P.nblocks ? (b0 + P.blocks_per_wg) : P.nblocks;
   const uint64_t s_lo = P.halo + (uint64_t)b0 * DF_BLOCK;
   const uint64_t s_hi = (P.halo + (uint64_t)b1 * DF_BLOCK) < P.end ? (P.halo + (uint64_t)b1 * DF_BLOCK) : P.end;
-  const uint64_t h_lo = s_lo > DF_MAXDIST ? s_lo - DF_MAXDIST : 0;
+  // a segment start (restart point) sees no history: its matches stay inside
+  // the segment, so inflate can decode segments independently
+  const bool restart = (b0 % P.restart) == 0 && (b0 > 0 || P.halo == 0);
+  const uint64_t h_lo = restart ? s_lo : (s_lo > DF_MAXDIST ? s_lo - DF_MAXDIST : 0);
   const uint8_t *g = P.base + h_lo;  // rel 0
   const uint32_t rs = (uint32_t)(s_lo - h_lo), re = (uint32_t)(s_hi - h_lo);
   const uint32_t rend = (uint32_t)(P.end - h_lo);  // bytes available (for hashing)
@@ -852,14 +858,26 @@ __global__ __launch_bounds__(DF_THREADS) void deflate_kernel(DeflateParams P) {
 }
 
 // ---- stitching: exclusive scan of block sizes, then a byte-exact gather ---------------------------
+// A restart point (segment boundary) is announced by two empty stored blocks
+// after the preceding block (which always ends byte-aligned):
+//   00 00 00 FF FF 00 00 00 FF FF
+// An ordinary block boundary carries at most one, so the 10-byte pattern at a
+// stored-block end marks a segment that inflate may decode on its own.
+constexpr uint32_t kRestartMarkerLen = 10;
+__device__ __forceinline__ bool restart_after(uint32_t b, uint32_t n, uint32_t restart, int final_) {
+  (void)final_;  // a call's last block is never followed by a restart (the next shard may use it as halo)
+  return (b + 1 < n) && ((b + 1) % restart) == 0;
+}
+
 __global__ __launch_bounds__(1024) void scan_sizes(const uint32_t *__restrict__ len, uint32_t n,
-                                                   uint64_t *__restrict__ off, uint64_t base) {
+                                                   uint64_t *__restrict__ off, uint64_t base, uint32_t restart,
+                                                   int final_) {
   __shared__ uint64_t part[1024];
   const uint32_t t = threadIdx.x;
   const uint32_t per = (n + 1023) / 1024;
   const uint32_t a = t * per, b = (a + per) < n ? (a + per) : n;
   uint64_t sum = 0;
-  for (uint32_t i = a; i < b; ++i) sum += len[i];
+  for (uint32_t i = a; i < b; ++i) sum += len[i] + (restart_after(i, n, restart, final_) ? kRestartMarkerLen : 0);
   part[t] = sum;
   __syncthreads();
   for (int d = 1; d < 1024; d <<= 1) {
@@ -871,17 +889,22 @@ __global__ __launch_bounds__(1024) void scan_sizes(const uint32_t *__restrict__ 
   uint64_t run = base + part[t] - sum;
   for (uint32_t i = a; i < b; ++i) {
     off[i] = run;
-    run += len[i];
+    run += len[i] + (restart_after(i, n, restart, final_) ? kRestartMarkerLen : 0);
   }
   if (t == 1023) off[n] = base + part[1023];
 }
 
 __global__ __launch_bounds__(256) void gather_blocks(const uint8_t *__restrict__ slots, const uint32_t *__restrict__ len,
-                                                     const uint64_t *__restrict__ off, uint8_t *__restrict__ out) {
+                                                     const uint64_t *__restrict__ off, uint8_t *__restrict__ out,
+                                                     uint32_t nblocks, uint32_t restart, int final_) {
   const uint32_t b = blockIdx.x;
   const uint8_t *src = slots + (size_t)b * DF_SLOT;
   uint8_t *dst = out + off[b];
   const uint32_t n = len[b];
+  if (restart_after(b, nblocks, restart, final_) && threadIdx.x < kRestartMarkerLen) {
+    const uint32_t i = threadIdx.x % 5;
+    dst[n + threadIdx.x] = i < 3 ? 0 : 0xFF;
+  }
   // destination-aligned 4-byte words built from the (aligned) source with a byte shift
   const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 3);
   const uint32_t head = mis ? 4 - mis : 0;
@@ -943,9 +966,28 @@ static DeflateLevel level_params(int level) {
 
 uint32_t *g_deflate_debug = nullptr;  // test hook (zt_debug_set_deflate_dump)
 
+// Work split: enough workgroups to cover every CU twice, at most 32 blocks
+// (1 MiB) per workgroup.  Returns the scratch bytes needed.
+static size_t deflate_geometry(const DeviceCtx *c, size_t n, uint32_t *nblocks, uint32_t *k, uint32_t *nwg,
+                               size_t *tok_bytes, size_t *slot_bytes, size_t *len_bytes, size_t *off_bytes) {
+  *nblocks = (uint32_t)((n + DF_BLOCK - 1) / DF_BLOCK);
+  if (*nblocks == 0) *nblocks = 1;
+  uint32_t kk = (*nblocks + 2 * c->num_cu - 1) / (2 * c->num_cu);
+  uint32_t k2 = 1;
+  while (k2 < kk && k2 < 32) k2 <<= 1;  // a power of two, so it divides the restart interval
+  kk = k2;
+  *k = kk;
+  *nwg = (*nblocks + kk - 1) / kk;
+  *tok_bytes = (size_t)*nwg * DF_BLOCK * 4;
+  *slot_bytes = (size_t)*nblocks * DF_SLOT;
+  *len_bytes = ((size_t)*nblocks * 4 + 255) & ~size_t(255);
+  *off_bytes = ((size_t)(*nblocks + 1) * 8 + 255) & ~size_t(255);
+  return *tok_bytes + *slot_bytes + *len_bytes + *off_bytes + 256;
+}
+
 size_t deflate_bound_bytes(size_t n) {
   size_t nb = (n + DF_BLOCK - 1) / DF_BLOCK;
-  return n + nb * 16 + 64;
+  return n + nb * 16 + (nb / kRestartBlocks + 1) * kRestartMarkerLen + 64;
 }
 
 int deflate_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t halo, int final_, int ctype, int level,
@@ -970,17 +1012,9 @@ int deflate_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t halo, in
     *out_len = 5;
     return ZT_OK;
   }
-  const uint32_t nblocks = (uint32_t)((n + DF_BLOCK - 1) / DF_BLOCK);
-  // enough workgroups to cover every CU a few times, at most 32 blocks (1 MiB) each
-  uint32_t k = (nblocks + 2 * c->num_cu - 1) / (2 * c->num_cu);
-  if (k < 1) k = 1;
-  if (k > 32) k = 32;
-  const uint32_t nwg = (nblocks + k - 1) / k;
-  const size_t tok_bytes = (size_t)nwg * DF_BLOCK * 4;
-  const size_t slot_bytes = (size_t)nblocks * DF_SLOT;
-  const size_t len_bytes = ((size_t)nblocks * 4 + 255) & ~size_t(255);
-  const size_t off_bytes = ((size_t)(nblocks + 1) * 8 + 255) & ~size_t(255);
-  const size_t need = tok_bytes + slot_bytes + len_bytes + off_bytes + 256;
+  uint32_t nblocks, k, nwg;
+  size_t tok_bytes, slot_bytes, len_bytes, off_bytes;
+  const size_t need = deflate_geometry(c, n, &nblocks, &k, &nwg, &tok_bytes, &slot_bytes, &len_bytes, &off_bytes);
   if (need > scratch_size) return set_error(ZT_E_NOMEM, "deflate scratch too small");
   uint8_t *sb = static_cast<uint8_t *>(scratch_base);
   DeflateParams P;
@@ -989,6 +1023,7 @@ int deflate_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t halo, in
   P.end = halo + n;
   P.blocks_per_wg = k;
   P.nblocks = nblocks;
+  P.restart = kRestartBlocks;
   P.final_ = final_;
   DeflateLevel L = level_params(level);
   P.max_chain = L.max_chain;
@@ -1001,27 +1036,26 @@ int deflate_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t halo, in
   P.slots = sb + tok_bytes;
   P.slot_len = reinterpret_cast<uint32_t *>(sb + tok_bytes + slot_bytes);
   uint64_t *off = reinterpret_cast<uint64_t *>(sb + tok_bytes + slot_bytes + len_bytes);
+  ZT_TRY(timing_begin(c, s));
   deflate_kernel<<<nwg, DF_THREADS, 0, s>>>(P);
   ZT_HIP(hipGetLastError());
-  scan_sizes<<<1, 1024, 0, s>>>(P.slot_len, nblocks, off, 0);
+  ZT_TRY(timing_end(c, s));
+  scan_sizes<<<1, 1024, 0, s>>>(P.slot_len, nblocks, off, 0, P.restart, final_);
   ZT_HIP(hipGetLastError());
-  gather_blocks<<<nblocks, 256, 0, s>>>(P.slots, P.slot_len, off, d_out);
+  gather_blocks<<<nblocks, 256, 0, s>>>(P.slots, P.slot_len, off, d_out, nblocks, P.restart, final_);
   ZT_HIP(hipGetLastError());
   uint64_t total = 0;
   ZT_HIP(hipMemcpyAsync(&total, off + nblocks, sizeof total, hipMemcpyDeviceToHost, s));
   ZT_HIP(hipStreamSynchronize(s));
+  ZT_TRY(timing_collect(c, &c->times.deflate_ms, &c->times.deflate_launches));
   *out_len = total;
   return ZT_OK;
 }
 
 size_t deflate_scratch_bytes(const DeviceCtx *c, size_t n) {
-  const uint32_t nblocks = (uint32_t)((n + DF_BLOCK - 1) / DF_BLOCK) + 1;
-  uint32_t k = (nblocks + 2 * c->num_cu - 1) / (2 * c->num_cu);
-  if (k < 1) k = 1;
-  if (k > 32) k = 32;
-  const uint32_t nwg = (nblocks + k - 1) / k + 1;
-  return (size_t)nwg * DF_BLOCK * 4 + (size_t)nblocks * DF_SLOT + (size_t)nblocks * 4 + 256 +
-         (size_t)(nblocks + 1) * 8 + 256 + 256;
+  uint32_t nb, k, nwg;
+  size_t a, b2, l, o;
+  return deflate_geometry(c, n, &nb, &k, &nwg, &a, &b2, &l, &o);
 }
 
 }  // namespace zt

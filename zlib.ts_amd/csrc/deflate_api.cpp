@@ -168,7 +168,20 @@ int zt_inflate_dev(zt_inflate_plan *plan, const void *d_in, size_t n, void *d_ou
   DeviceCtx *c;
   ZT_TRY(get_ctx(&c));
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-  InfJob job{(const uint8_t *)d_in, n, 0, (uint8_t *)d_out, out_cap, 0, 0};
+  uint8_t *o = (uint8_t *)d_out;
+  size_t ol = 0, eip = 0;
+  const int seg = inflate_segments_dev(c, (const uint8_t *)d_in, n, 0, &o, out_cap, &ol, &eip, s);
+  if (seg < 0) return seg;
+  if (seg == 0) {
+    *out_len = ol;
+    if (end_ip) *end_ip = eip;
+    return ZT_OK;
+  }
+  InfJob job{};
+  job.in = (const uint8_t *)d_in;
+  job.n = n;
+  job.out = (uint8_t *)d_out;
+  job.cap = out_cap;
   InfJob *dj = (InfJob *)plan->jobs;
   InfResult *dr = (InfResult *)((uint8_t *)plan->jobs + 256);
   ZT_HIP(hipMemcpyAsync(dj, &job, sizeof job, hipMemcpyHostToDevice, s));

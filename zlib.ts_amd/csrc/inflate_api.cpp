@@ -69,8 +69,13 @@ static int inflate_host_batch(const uint8_t *const *in, const size_t *n, const s
     ZT_TRY(scratch(c, 1, out_total, &d_out));
     for (size_t k = 0; k < todo.size(); ++k) {
       size_t i = todo[k];
-      jobs[k] = InfJob{(const uint8_t *)d_in + in_off[i], n[i], index ? index[i] : 0,
-                       (uint8_t *)d_out + out_off[k], cap[i], strict, 0};
+      jobs[k] = InfJob{};
+      jobs[k].in = (const uint8_t *)d_in + in_off[i];
+      jobs[k].n = n[i];
+      jobs[k].start = index ? index[i] : 0;
+      jobs[k].out = (uint8_t *)d_out + out_off[k];
+      jobs[k].cap = cap[i];
+      jobs[k].strict = strict;
     }
     ZT_HIP(hipMemcpyAsync(d_jobs, jobs.data(), todo.size() * sizeof(InfJob), hipMemcpyHostToDevice, c->stream));
     ZT_TRY(inflate_jobs_dev((const InfJob *)d_jobs, (InfResult *)d_res, (int)todo.size(), c->stream));
@@ -118,6 +123,28 @@ extern "C" {
 int zt_inflate_raw(const uint8_t *in, size_t n, size_t index, const zt_inflate_opts *opts, uint8_t **out,
                    size_t *out_len, size_t *end_ip) {
   if (!out || !out_len) return set_error(ZT_E_ARG, "null output");
+  if (!(opts && opts->ref_strict) && in && n >= index + (1u << 18)) {
+    // large stream: segment-parallel decode when it carries restart points
+    DeviceCtx *c;
+    ZT_TRY(get_ctx(&c));
+    void *d_in;
+    ZT_TRY(scratch(c, 0, n, &d_in));
+    ZT_HIP(hipMemcpyAsync(d_in, in, n, hipMemcpyHostToDevice, c->stream));
+    uint8_t *d_out = nullptr;
+    size_t ol = 0, eip = 0;
+    const int seg = inflate_segments_dev(c, (const uint8_t *)d_in, n, index, &d_out, 0, &ol, &eip, c->stream);
+    if (seg < 0) return seg;
+    if (seg == 0) {
+      uint8_t *h = (uint8_t *)malloc(ol ? ol : 1);
+      if (!h) return set_error(ZT_E_NOMEM, "host allocation failed");
+      if (ol) ZT_HIP(hipMemcpyAsync(h, d_out, ol, hipMemcpyDeviceToHost, c->stream));
+      ZT_HIP(hipStreamSynchronize(c->stream));
+      *out = h;
+      *out_len = ol;
+      if (end_ip) *end_ip = eip;
+      return ZT_OK;
+    }
+  }
   int st = 0;
   size_t ip = 0;
   const uint8_t *p = in;

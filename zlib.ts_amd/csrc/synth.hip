@@ -1,0 +1,100 @@
+// synth.hip -- synthetic corpora for benchmarks and tests.
+// Piece i (64 KiB) of a buffer is generator `kind` seeded with seed + i, so a
+// piece equals tools/gen_golden.mjs / oracle zo_gen(kind, seed + i, 65536).
+// kind 3 ("mixed") cycles wordsalad / xorshift32 / structured per 4 MiB window.
+#include "zt_internal.h"
+
+namespace zt {
+namespace {
+
+constexpr uint32_t kPieceBytes = 65536;
+
+__device__ __forceinline__ uint32_t xs32(uint32_t x) {
+  x ^= x << 13;
+  x ^= x >> 17;
+  x ^= x << 5;
+  return x;
+}
+
+struct WordOut {
+  uint32_t *w;
+  uint32_t acc = 0, k = 0, i = 0, n;
+  __device__ void put(uint32_t b) {
+    acc |= b << (8 * k);
+    if (++k == 4) {
+      w[i >> 2] = acc;
+      acc = 0;
+      k = 0;
+    }
+    ++i;
+  }
+  __device__ void finish(uint8_t *bytes) {
+    for (uint32_t j = 0; j < k; ++j) bytes[(i - k) + j] = (uint8_t)(acc >> (8 * j));
+  }
+};
+
+__global__ __launch_bounds__(64) void synth_kernel(int kind, uint32_t seed, uint8_t *out, uint64_t n) {
+  const uint64_t piece = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+  const uint64_t lo = piece * kPieceBytes;
+  if (lo >= n) return;
+  const uint32_t len = (uint32_t)((n - lo) < kPieceBytes ? (n - lo) : kPieceBytes);
+  int k = kind;
+  if (kind == 3) {
+    const int m = (int)((piece >> 6) % 3);
+    k = m == 0 ? 1 : m == 1 ? 0 : 2;
+  }
+  uint32_t x = seed + (uint32_t)piece;
+  if (x == 0) x = 0x9E3779B9u;
+  WordOut o;
+  o.w = reinterpret_cast<uint32_t *>(out + lo);
+  o.n = len;
+  if (k == 0) {
+    for (uint32_t i = 0; i < len; ++i) {
+      x = xs32(x);
+      o.put(x & 0xFF);
+    }
+  } else if (k == 1) {
+    // 16-word vocabulary, packed: offsets and lengths (the, of, and, deflate, ...)
+    const char vocab[] = "theofanddeflatehuffmanwindowstreamblocklz77matchliteralinflategpuwavelanechunk";
+    const uint8_t voff[16] = {0, 3, 5, 8, 15, 22, 28, 34, 39, 43, 48, 55, 62, 65, 69, 73};
+    const uint8_t vlen[16] = {3, 2, 3, 7, 7, 6, 6, 5, 4, 5, 7, 7, 3, 4, 4, 5};
+    while (o.i < len) {
+      x = xs32(x);
+      const uint32_t w = x & 15;
+      for (uint32_t j = 0; j < vlen[w] && o.i < len; ++j) o.put((uint8_t)vocab[voff[w] + j]);
+      if (((x >> 4) & 15) == 0) {
+        if (o.i < len) o.put('.');
+        if (o.i < len) o.put('\n');
+      } else if (o.i < len) {
+        o.put(' ');
+      }
+    }
+  } else {
+    int32_t v = 0;
+    for (uint32_t i = 0; i < len; i += 4) {
+      x = xs32(x);
+      v = (int32_t)((uint32_t)v + (uint32_t)((int32_t)(x & 0xFF) - 128));
+      for (uint32_t b = 0; b < 4 && i + b < len; ++b) o.put(((uint32_t)v >> (8 * b)) & 0xFF);
+    }
+  }
+  o.finish(out + lo);
+}
+
+}  // namespace
+}  // namespace zt
+
+using namespace zt;
+
+extern "C" int zt_synth_dev(int kind, uint32_t seed, void *d_out, size_t n, void *stream) {
+  if (kind < 0 || kind > 3) return set_error(ZT_E_ARG, "unknown generator");
+  if (n == 0) return ZT_OK;
+  if (!d_out) return set_error(ZT_E_ARG, "null output");
+  if (reinterpret_cast<uintptr_t>(d_out) & 3) return set_error(ZT_E_ARG, "output must be 4-byte aligned");
+  DeviceCtx *c;
+  ZT_TRY(get_ctx(&c));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  const uint64_t pieces = (n + kPieceBytes - 1) / kPieceBytes;
+  synth_kernel<<<(unsigned)((pieces + 63) / 64), 64, 0, s>>>(kind, seed, static_cast<uint8_t *>(d_out), n);
+  ZT_HIP(hipGetLastError());
+  return ZT_OK;
+}

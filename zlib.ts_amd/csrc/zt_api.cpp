@@ -28,6 +28,27 @@ int hip_fail(hipError_t e, const char *what) {
   return set_error(ZT_E_HIP, buf);
 }
 
+int timing_begin(DeviceCtx *c, hipStream_t s) {
+  if (!c->timing) return ZT_OK;
+  ZT_HIP(hipEventRecord(c->ev[0], s));
+  return ZT_OK;
+}
+
+int timing_end(DeviceCtx *c, hipStream_t s) {
+  if (!c->timing) return ZT_OK;
+  ZT_HIP(hipEventRecord(c->ev[1], s));
+  return ZT_OK;
+}
+
+int timing_collect(DeviceCtx *c, double *acc_ms, uint64_t *count) {
+  if (!c->timing) return ZT_OK;
+  float ms = 0;
+  ZT_HIP(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+  *acc_ms += ms;
+  ++*count;
+  return ZT_OK;
+}
+
 static std::mutex g_mu;
 static std::vector<DeviceCtx *> g_ctx;
 
@@ -52,6 +73,8 @@ int get_ctx(DeviceCtx **out) {
     ZT_HIP(hipMalloc(&c->d_crc_x2n, sizeof x2n));
     ZT_HIP(hipMemcpy(c->d_crc_nib, nib, sizeof nib, hipMemcpyHostToDevice));
     ZT_HIP(hipMemcpy(c->d_crc_x2n, x2n, sizeof x2n, hipMemcpyHostToDevice));
+    ZT_HIP(hipEventCreate(&c->ev[0]));
+    ZT_HIP(hipEventCreate(&c->ev[1]));
     g_ctx[g_dev] = c;
   }
   *out = g_ctx[g_dev];
@@ -151,6 +174,22 @@ int zt_adler32_update(uint32_t adler, const uint8_t *data, size_t len, uint32_t 
 int zt_checksums(const uint8_t *data, size_t len, uint32_t crc_in, uint32_t adler_in, uint32_t *crc_out,
                  uint32_t *adler_out) {
   return checksums_host(data, len, crc_in, adler_in, crc_out, adler_out);
+}
+
+int zt_timing_enable(int on) {
+  DeviceCtx *c;
+  ZT_TRY(get_ctx(&c));
+  c->timing = on != 0;
+  c->times = zt_kernel_times{};
+  return ZT_OK;
+}
+
+int zt_timing_read(zt_kernel_times *out) {
+  if (!out) return set_error(ZT_E_ARG, "null output");
+  DeviceCtx *c;
+  ZT_TRY(get_ctx(&c));
+  *out = c->times;
+  return ZT_OK;
 }
 
 }  // extern "C"

@@ -37,11 +37,21 @@ struct DeviceCtx {
   uint32_t *d_crc_nib = nullptr;    // 16 x 16 nibble tables (slice-by-8)
   uint32_t *d_crc_x2n = nullptr;    // x^(2^k) mod P, k = 0..31
   // scratch
-  void *d_buf[4] = {nullptr, nullptr, nullptr, nullptr};
-  size_t buf_size[4] = {0, 0, 0, 0};
+  void *d_buf[8] = {};
+  size_t buf_size[8] = {};
   void *h_pinned = nullptr;
+  // zt_timing_enable: HIP-event kernel timing
+  bool timing = false;
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  zt_kernel_times times = {};
   size_t pinned_size = 0;
 };
+
+// Records ev[0] (begin) / ev[1] (end) around a launch when timing is on.
+int timing_begin(DeviceCtx *c, hipStream_t s);
+int timing_end(DeviceCtx *c, hipStream_t s);
+// After the stream is synchronized: adds the elapsed time to *acc.
+int timing_collect(DeviceCtx *c, double *acc_ms, uint64_t *count);
 
 // Context of the calling thread's current device (created on first use).
 int get_ctx(DeviceCtx **out);
@@ -77,6 +87,27 @@ __host__ __device__ inline uint32_t x2nmodp(const uint32_t *x2n, uint64_t n, uns
   return p;
 }
 
+// RFC 1951 3.2.5 length / distance code arithmetic, ALU only (table lookups
+// indexed by non-provably-uniform values become dependent global loads).
+__host__ __device__ __forceinline__ uint32_t len_base(uint32_t ls) {  // ls = symbol - 257, 0..28
+  if (ls < 8) return ls + 3;
+  if (ls >= 28) return 258;
+  uint32_t e = (ls >> 2) - 1;
+  return ((4 + (ls & 3)) << e) + 3;
+}
+__host__ __device__ __forceinline__ uint32_t len_extra(uint32_t ls) {
+  return (ls < 8 || ls >= 28) ? 0 : (ls >> 2) - 1;
+}
+__host__ __device__ __forceinline__ uint32_t dist_base(uint32_t ds) {  // 0..29
+  if (ds < 4) return ds + 1;
+  uint32_t e = (ds >> 1) - 1;
+  return ((2 + (ds & 1)) << e) + 1;
+}
+__host__ __device__ __forceinline__ uint32_t dist_extra(uint32_t ds) { return ds < 4 ? 0 : (ds >> 1) - 1; }
+
+typedef __attribute__((address_space(1))) const uint8_t g_u8;
+typedef __attribute__((address_space(1))) const uint32_t g_u32;
+
 void crc_host_tables(uint32_t byte_table[256], uint32_t nib[256], uint32_t x2n[32]);
 
 // ---- launchers (device-resident) ------------------------------------------------
@@ -91,7 +122,9 @@ struct InfJob {
   uint8_t *out;       // output buffer (device)
   uint64_t cap;       // output capacity; decoding continues past it, counting only
   int32_t strict;     // stop with 'input buffer is broken' where the reference's EOF test throws
-  int32_t pad;
+  uint32_t stop_first;        // segment decode: first candidate index to test
+  const uint64_t *stops;      // sorted segment starts (byte positions in `in`), or null
+  uint64_t stop_count;
 };
 
 struct InfResult {
@@ -100,8 +133,14 @@ struct InfResult {
   int32_t status;
   int32_t detail;       // code length / BTYPE for the message
   int32_t strict_fail;  // reference's readBits EOF check would throw
-  int32_t pad;
+  int32_t stop_idx;     // segment decode: index of the segment start where decoding stopped, -1 at BFINAL
 };
+
+// segment-parallel inflate (restart markers written by deflate); returns 1 when
+// the stream has no usable segments (caller decodes it with one wave)
+// (*d_out_io null: the output goes to scratch slot 1, returned in *d_out_io)
+int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t index, uint8_t **d_out_io,
+                         size_t out_cap, size_t *out_len, size_t *end_ip, hipStream_t s);
 
 int inflate_jobs_dev(const InfJob *d_jobs, InfResult *d_res, int count, hipStream_t s);
 int inflate_error(int status, int detail);

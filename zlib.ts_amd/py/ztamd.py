@@ -30,6 +30,11 @@ class DeflateOpts(ctypes.Structure):
     _fields_ = [("compression_type", ctypes.c_int), ("lazy", ctypes.c_int), ("level", ctypes.c_int)]
 
 
+class KernelTimes(ctypes.Structure):
+    _fields_ = [("deflate_ms", ctypes.c_double), ("deflate_launches", ctypes.c_uint64),
+                ("inflate_ms", ctypes.c_double), ("inflate_launches", ctypes.c_uint64)]
+
+
 class InflateOpts(ctypes.Structure):
     _fields_ = [("buffer_type", ctypes.c_int), ("buffer_size", ctypes.c_size_t), ("ref_strict", ctypes.c_int)]
 
@@ -70,6 +75,9 @@ def _load():
         "zt_inflate_plan_create": ([sz, sz, P(vp)], ctypes.c_int),
         "zt_inflate_plan_destroy": ([vp], None),
         "zt_inflate_dev": ([vp, vp, sz, vp, sz, P(sz), P(sz), vp], ctypes.c_int),
+        "zt_synth_dev": ([ctypes.c_int, u32, vp, sz, vp], ctypes.c_int),
+        "zt_timing_enable": ([ctypes.c_int], ctypes.c_int),
+        "zt_timing_read": ([P(KernelTimes)], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name, None)
@@ -88,6 +96,7 @@ SYMBOLS = [
     "zt_adler32_update", "zt_checksums", "zt_deflate_raw", "zt_inflate_raw", "zt_inflate_raw_batch",
     "zt_deflate_raw_batch", "zt_dev_checksums", "zt_deflate_plan_create", "zt_deflate_plan_destroy",
     "zt_deflate_bound", "zt_deflate_dev", "zt_inflate_plan_create", "zt_inflate_plan_destroy", "zt_inflate_dev",
+    "zt_synth_dev", "zt_timing_enable", "zt_timing_read",
 ]
 
 
@@ -215,7 +224,7 @@ class DeflatePlan:
         return olen.value
 
     def close(self):
-        if self.h:
+        if self.h and lib is not None:
             lib.zt_deflate_plan_destroy(self.h)
             self.h = ctypes.c_void_p()
 
@@ -233,7 +242,7 @@ class InflatePlan:
         return olen.value, ip.value
 
     def close(self):
-        if self.h:
+        if self.h and lib is not None:
             lib.zt_inflate_plan_destroy(self.h)
             self.h = ctypes.c_void_p()
 
@@ -242,3 +251,23 @@ class InflatePlan:
 
 def deflate_bound(n):
     return lib.zt_deflate_bound(n)
+
+
+GEN_KINDS = {"xorshift32": 0, "wordsalad": 1, "structured": 2, "mixed": 3}
+
+
+def synth_dev(kind, seed, ptr, n, stream=None):
+    """Fill device memory with a synthetic corpus (64 KiB piece i = generator
+    seeded with seed + i)."""
+    _check(lib.zt_synth_dev(GEN_KINDS.get(kind, kind), seed, ptr, n, stream))
+
+
+def timing_enable(on=True):
+    _check(lib.zt_timing_enable(1 if on else 0))
+
+
+def timing_read():
+    t = KernelTimes()
+    _check(lib.zt_timing_read(ctypes.byref(t)))
+    return {"deflate_ms": t.deflate_ms, "deflate_launches": t.deflate_launches,
+            "inflate_ms": t.inflate_ms, "inflate_launches": t.inflate_launches}
