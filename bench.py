@@ -35,6 +35,8 @@ sys.path.insert(0, os.path.join(HERE, "zlib.ts_amd", "py"))
 
 import torch  # noqa: E402
 
+from zt_shard import max_over_ranks  # noqa: E402
+
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 WINDOW = 4 << 20
 KINDS = ["wordsalad", "xorshift32", "structured"]  # mixed corpus order per 4 MiB window
@@ -132,10 +134,7 @@ def main():
     elapsed = time.perf_counter() - t0
     kt = zt.timing_read()
     zt.timing_enable(False)
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(elapsed, dist, device="cuda")
 
     value = world * n * args.steps / elapsed / 2**30
     ms_step = elapsed / args.steps * 1e3

@@ -787,8 +787,25 @@ __device__ void encode_block(DefShared *s, const DeflateParams &P, const uint32_
   __syncthreads();
 }
 
+#ifdef ZT_DF_PROF
+__device__ unsigned long long g_df_prof[8];
+#define DFP_T() ((uint64_t)__builtin_readcyclecounter())
+#define DFP_MARK(i)                    \
+  do {                                 \
+    const uint64_t now_ = DFP_T();     \
+    prof[i] += now_ - prof_t;          \
+    prof_t = now_;                     \
+  } while (0)
+#else
+#define DFP_MARK(i) ((void)0)
+#endif
+
 __global__ __launch_bounds__(DF_THREADS) void deflate_kernel(DeflateParams P) {
   __shared__ DefShared s;
+#ifdef ZT_DF_PROF
+  uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t prof_t = DFP_T();
+#endif
   const uint32_t t = threadIdx.x;
   const uint32_t wg = blockIdx.x;
   const uint32_t b0 = wg * P.blocks_per_wg;
@@ -831,14 +848,18 @@ __global__ __launch_bounds__(DF_THREADS) void deflate_kernel(DeflateParams P) {
     __syncthreads();
     uint32_t ih = p1 - 2 < rend - 2 ? p1 - 2 : rend - 2;
     if (p1 < 2) ih = 0;
+    DFP_MARK(0);
     if (ih > inserted) {
       chain_build(&s, inserted, ih);
       inserted = ih;
     }
+    DFP_MARK(1);
     search_sub(&s, P, p0, p1, 0);
     __syncthreads();
+    DFP_MARK(2);
     if (t < 64) parse_sub(&s, P, p0, p1, tok);
     __syncthreads();
+    DFP_MARK(3);
     if (p1 - blk_lo == DF_BLOCK || p1 == re) {
       // finish block `blk` covering [blk_lo, p1)
       const uint32_t blen = p1 - blk_lo;
@@ -846,7 +867,9 @@ __global__ __launch_bounds__(DF_THREADS) void deflate_kernel(DeflateParams P) {
       if (t < 64) plan_block(&s, P, blen);
       __syncthreads();
       __threadfence_block();
+      DFP_MARK(4);
       encode_block(&s, P, tok, s.ntok, P.slots + (size_t)blk * DF_SLOT, P.slot_len + blk, g + blk_lo, blen, last);
+      DFP_MARK(5);
       for (uint32_t i = t; i < 288; i += DF_THREADS) s.lit_hist[i] = 0;
       if (t < 32) s.dist_hist[t] = 0;
       if (t == 0) s.ntok = 0;
@@ -855,6 +878,10 @@ __global__ __launch_bounds__(DF_THREADS) void deflate_kernel(DeflateParams P) {
       blk_lo = p1;
     }
   }
+#ifdef ZT_DF_PROF
+  if (t == 0)
+    for (int i = 0; i < 8; ++i) atomicAdd(&g_df_prof[i], (unsigned long long)prof[i]);
+#endif
 }
 
 // ---- stitching: exclusive scan of block sizes, then a byte-exact gather ---------------------------
@@ -864,9 +891,10 @@ __global__ __launch_bounds__(DF_THREADS) void deflate_kernel(DeflateParams P) {
 // An ordinary block boundary carries at most one, so the 10-byte pattern at a
 // stored-block end marks a segment that inflate may decode on its own.
 constexpr uint32_t kRestartMarkerLen = 10;
+// (a non-final call -- a shard -- also ends with the marker: the next shard
+// is independent when deflated with halo 0, see zt_shard.py)
 __device__ __forceinline__ bool restart_after(uint32_t b, uint32_t n, uint32_t restart, int final_) {
-  (void)final_;  // a call's last block is never followed by a restart (the next shard may use it as halo)
-  return (b + 1 < n) && ((b + 1) % restart) == 0;
+  return (b + 1 < n) ? ((b + 1) % restart) == 0 : !final_;
 }
 
 __global__ __launch_bounds__(1024) void scan_sizes(const uint32_t *__restrict__ len, uint32_t n,
@@ -1051,6 +1079,15 @@ int deflate_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t halo, in
   *out_len = total;
   return ZT_OK;
 }
+
+#ifdef ZT_DF_PROF
+extern "C" int zt_debug_deflate_prof(unsigned long long *out) {
+  hipMemcpyFromSymbol(out, HIP_SYMBOL(g_df_prof), sizeof(unsigned long long) * 8);
+  unsigned long long z[8] = {};
+  hipMemcpyToSymbol(HIP_SYMBOL(g_df_prof), z, sizeof z);
+  return 0;
+}
+#endif
 
 size_t deflate_scratch_bytes(const DeviceCtx *c, size_t n) {
   uint32_t nb, k, nwg;
