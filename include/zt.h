@@ -131,7 +131,8 @@ int zt_inflate_dev(zt_inflate_plan *plan, const void *d_in, size_t n, void *d_ou
 /* ---- benchmark / test support (no reference counterpart) ---- */
 /* Synthetic corpus: 64 KiB piece i is generator `kind`
  * (0 xorshift32, 1 wordsalad, 2 structured int32 deltas, 3 mixed per 4 MiB
- * window) seeded with seed + i.  d_out must be 4-byte aligned. */
+ * window) seeded with seed + i.  d_out must be 4-byte aligned.  With a
+ * null stream the call returns when the data is written. */
 int zt_synth_dev(int kind, uint32_t seed, void *d_out, size_t n, void *stream);
 /* Kernel-time accounting with HIP events on the launch stream: the deflate
  * LZ77/Huffman kernel and the inflate decode kernel of the device paths. */

@@ -1,0 +1,43 @@
+// Runs the JS facade (zlib.ts_amd/lib) over cases prepared by
+// tests/test_js_facade.py and prints one JSON result per case.
+import fs from 'fs';
+import { RawDeflate, RawInflate, CRC32, Adler32, deviceCount } from '../../zlib.ts_amd/lib/index.js';
+
+const hex = (s) => Uint8Array.from(Buffer.from(s, 'hex'));
+const tohex = (a) => Buffer.from(a.buffer, a.byteOffset, a.length).toString('hex');
+const cases = JSON.parse(fs.readFileSync(process.argv[2], 'utf8'));
+const out = [];
+for (const c of cases) {
+    const r = { id: c.id };
+    try {
+        if (c.op === 'devices') {
+            r.value = deviceCount();
+        } else if (c.op === 'crc32') {
+            r.value = c.crc === undefined ? CRC32.create(hex(c.in), c.pos, c.length) : CRC32.update(hex(c.in), c.crc, c.pos, c.length);
+        } else if (c.op === 'adler32') {
+            r.value = c.str !== undefined ? Adler32.create(c.str) : Adler32.update(c.adler === undefined ? 1 : c.adler, hex(c.in), c.len, c.pos);
+        } else if (c.op === 'inflate') {
+            const inf = new RawInflate(hex(c.in), { index: c.index || 0, refStrict: !!c.strict, bufferType: c.bufferType === undefined ? 1 : c.bufferType });
+            const o = inf.decompress();
+            r.out = tohex(o);
+            r.ip = inf.ip;
+        } else if (c.op === 'deflate') {
+            const opts = Object.assign({}, c.opts || {});
+            if (c.prefix !== undefined) {
+                opts.outputBuffer = hex(c.prefix);
+                opts.outputIndex = c.prefix.length / 2;
+            }
+            const d = new RawDeflate(hex(c.in), opts);
+            const s = d.compress();
+            r.out = tohex(s);
+            r.op = d.op;
+            const body = s.subarray(opts.outputIndex || 0);
+            const back = new RawInflate(body, { refStrict: true }).decompress();
+            r.back = tohex(back);
+        }
+    } catch (e) {
+        r.error = typeof e === 'string' ? { string: e } : { message: e.message, status: e.ztStatus };
+    }
+    out.push(r);
+}
+console.log(JSON.stringify(out));

@@ -1,0 +1,132 @@
+"""The Node host side (zlib.ts_amd/lib over the N-API addon zt.node): the
+reference's RawDeflate / RawInflate / CRC32 / Adler32 surface, driven from
+Node exactly as the reference's callers would, checked against the golden
+vectors the reference produced (tests/golden) and the oracle."""
+import json
+import os
+import shutil
+import subprocess
+import tempfile
+import zlib
+
+import pytest
+
+from golden_util import blob_bytes, blob_matches, load, make_input
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NODE = shutil.which("node")
+ADDON = os.path.join(ROOT, "zlib.ts_amd", "zt.node")
+pytestmark = pytest.mark.skipif(not NODE or not os.path.exists(ADDON), reason="node or zt.node missing")
+
+
+def s_of(c):
+    return bytes.fromhex(c["in"])[c["index"]:]
+
+
+def run_cases(cases):
+    with tempfile.NamedTemporaryFile("w", suffix=".json", delete=False) as f:
+        json.dump(cases, f)
+        path = f.name
+    try:
+        p = subprocess.run([NODE, os.path.join(ROOT, "tests", "js", "facade_check.mjs"), path],
+                           capture_output=True, text=True, timeout=600)
+    finally:
+        os.unlink(path)
+    assert p.returncode == 0, p.stderr
+    return {r["id"]: r for r in json.loads(p.stdout.strip().splitlines()[-1])}
+
+
+def test_facade_loads_and_refuses_without_gpu():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("CPU-only check")
+    res = run_cases([{"id": "n", "op": "devices"}, {"id": "c", "op": "crc32", "in": "313233"},
+                     {"id": "d", "op": "deflate", "in": "616263"}])
+    assert res["n"]["value"] == 0
+    assert res["c"]["error"]["status"] == -100
+    assert res["d"]["error"]["status"] == -100
+
+
+@pytest.mark.gpu
+def test_facade_checksums_golden(oracle):
+    g = load("checksums.json")
+    cases = []
+    for i, rec in enumerate(g["records"]):
+        data = make_input(rec["input"], oracle)
+        if len(data) > 4 << 20:
+            continue
+        cases.append({"id": f"c{i}", "op": "crc32", "in": data.hex(), "want": rec["crc32"]})
+        cases.append({"id": f"a{i}", "op": "adler32", "in": data.hex(), "want": rec["adler32"]})
+    for i, rec in enumerate(g.get("strings", [])):
+        if "adler32" in rec and "str" in rec:
+            cases.append({"id": f"s{i}", "op": "adler32", "str": rec["str"], "want": rec["adler32"]})
+    # CRC32.update quirk: length defaults to data.length even when pos > 0
+    d = oracle.gen("xorshift32", 5, 1000)
+    cases.append({"id": "q1", "op": "crc32", "in": d.hex(), "crc": 0, "pos": 100,
+                  "want": oracle.crc32(d[100:] + b"\0" * 100)})
+    cases.append({"id": "q2", "op": "crc32", "in": d.hex(), "crc": 0x12345678, "pos": 10, "length": 50,
+                  "want": oracle.crc32(d[10:60], 0x12345678)})
+    res = run_cases(cases)
+    for c in cases:
+        assert res[c["id"]].get("value") == c["want"], (c["id"], res[c["id"]])
+
+
+@pytest.mark.gpu
+def test_facade_inflate_golden(oracle):
+    cases = []
+    for i, rec in enumerate(load("inflate.json")["records"]):
+        s = blob_bytes(rec["stream"])
+        if s is None or len(s) > 1 << 20:
+            continue
+        c = {"id": f"i{i}", "op": "inflate", "in": s.hex(), "index": rec["opts"].get("index", 0), "strict": True,
+             "bufferType": rec["opts"].get("bufferType", 1)}
+        cases.append((c, rec))
+    res = run_cases([c for c, _ in cases])
+    checked = 0
+    for c, rec in cases:
+        r = res[c["id"]]
+        if "error" in rec:
+            assert r.get("error", {}).get("message") == rec["error"], (c["id"], r)
+            continue
+        assert "error" not in r, (c["id"], r)
+        out = bytes.fromhex(r["out"])
+        if c["bufferType"] == 0 and len(out) > 32768:
+            # documented divergence: the reference's BLOCK mode corrupts outputs > 32 KiB
+            assert out == zlib.decompress(s_of(c), -15)
+        else:
+            assert blob_matches(rec["out"], out), c["id"]
+        assert r["ip"] == rec["ip"]
+        checked += 1
+    assert checked > 20
+
+
+@pytest.mark.gpu
+def test_facade_deflate_roundtrip(oracle):
+    cases = []
+    inputs = [b"", b"a", b"abcdeabcX", oracle.gen("wordsalad", 1, 70000), oracle.gen("xorshift32", 2, 40000),
+              oracle.gen("structured", 3, 100000)]
+    for i, d in enumerate(inputs):
+        for ct in (0, 1, 2):
+            cases.append({"id": f"d{i}_{ct}", "op": "deflate", "in": d.hex(), "opts": {"compressionType": ct}})
+        cases.append({"id": f"p{i}", "op": "deflate", "in": d.hex(), "prefix": "1f8b0800"})
+    cases.append({"id": "bad", "op": "deflate", "in": "00", "opts": {"compressionType": 3}})
+    res = run_cases(cases)
+    for c in cases:
+        r = res[c["id"]]
+        if c["id"] == "bad":
+            assert r["error"] == {"string": "invalid compression type"}
+            continue
+        d = bytes.fromhex(c["in"])
+        ct = c.get("opts", {}).get("compressionType", 2)
+        if ct == 0 and not d:
+            continue  # the reference returns its untouched 32 KiB buffer here
+        out = bytes.fromhex(r["out"])
+        assert r["op"] == len(out)
+        if "prefix" in c:
+            assert out.startswith(bytes.fromhex(c["prefix"]))
+            out = out[4:]
+        assert zlib.decompress(out, -15) == d
+        assert bytes.fromhex(r["back"]) == d
+        o, ip = oracle.raw_inflate(out)
+        assert o == d and ip == len(out)

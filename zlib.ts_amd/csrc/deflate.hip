@@ -115,7 +115,12 @@ __device__ __forceinline__ uint32_t ld32(const DefShared *s, uint32_t rel) {
   uint32_t w = i >> 2;
   return __builtin_amdgcn_alignbyte(s->ring[w + 1], s->ring[w], i & 3);
 }
-__device__ __forceinline__ uint32_t hash3(uint32_t v) { return ((v & 0xFFFFFFu) * 0x9E3779B1u) >> (32 - DF_HBITS); }
+// chains link positions whose first DF_MINH (3 or 4) bytes hash alike
+#ifndef DF_MINH
+#define DF_MINH 3
+#endif
+constexpr uint32_t kKeyMask = DF_MINH >= 4 ? 0xFFFFFFFFu : 0xFFFFFFu;
+__device__ __forceinline__ uint32_t hash3(uint32_t v) { return ((v & kKeyMask) * 0x9E3779B1u) >> (32 - DF_HBITS); }
 
 __device__ __forceinline__ uint64_t lanemask_lt(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
 
@@ -226,14 +231,14 @@ __device__ void search_sub(DefShared *s, const DeflateParams &P, uint32_t p0, ui
           if (p - q > DF_MAXDIST || q < lo_bound) break;
           ++hops;
           link = s->prev[ridx(q)];
-          if (((ld32(s, q) ^ cur) & 0xFFFFFFu) != 0) continue;
+          if (((ld32(s, q) ^ cur) & kKeyMask) != 0) continue;
           if (best_len >= max_len) break;
           if (best_len >= 4) {
             // a candidate can only beat best_len if the 4 bytes ending there match
             const uint32_t o = best_len - 3;
             if (ld32(s, q + o) != ld32(s, p + o)) continue;
           }
-          uint32_t len = 3;
+          uint32_t len = DF_MINH;
           while (len < max_len) {
             uint32_t x = ld32(s, q + len) ^ ld32(s, p + len);
             if (x) {

@@ -96,5 +96,6 @@ extern "C" int zt_synth_dev(int kind, uint32_t seed, void *d_out, size_t n, void
   const uint64_t pieces = (n + kPieceBytes - 1) / kPieceBytes;
   synth_kernel<<<(unsigned)((pieces + 63) / 64), 64, 0, s>>>(kind, seed, static_cast<uint8_t *>(d_out), n);
   ZT_HIP(hipGetLastError());
+  if (!stream) ZT_HIP(hipStreamSynchronize(s));  // library stream: complete before returning
   return ZT_OK;
 }

@@ -1,0 +1,8 @@
+// zlib.ts_amd: the reference's hot-path classes over the MI355X engine.
+export { RawDeflate, CompressionType } from './RawDeflate.js';
+export { RawInflate, BufferType } from './RawInflate.js';
+export { CRC32 } from './CRC32.js';
+export { Adler32 } from './Adler32.js';
+import native from './native.js';
+export const deviceCount = () => native.deviceCount();
+export const version = () => native.version();

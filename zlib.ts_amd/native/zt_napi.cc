@@ -1,0 +1,193 @@
+// zt_napi.cc -- N-API addon: the thin binding between the JS facade
+// (zlib.ts_amd/lib/*.js, the reference's RawDeflate / RawInflate / CRC32 /
+// Adler32 surface) and libzt.so's C-ABI (include/zt.h).  Uint8Array memory is
+// passed zero-copy; results come back as new Uint8Arrays.  Every call runs on
+// the GPU; errors carry libzt's status code and message (the JS facade maps
+// them onto the reference's thrown values).
+#include <node_api.h>
+
+#include <cstdio>
+#include <cstring>
+
+#include "../../include/zt.h"
+
+namespace {
+
+napi_value throw_zt(napi_env env, int code) {
+  const char *msg = zt_last_error_message();
+  char codebuf[16];
+  snprintf(codebuf, sizeof codebuf, "%d", code);
+  napi_value err, m, c;
+  napi_create_string_utf8(env, msg ? msg : "libzt error", NAPI_AUTO_LENGTH, &m);
+  napi_create_string_utf8(env, codebuf, NAPI_AUTO_LENGTH, &c);
+  napi_create_error(env, c, m, &err);
+  napi_value num;
+  napi_create_int32(env, code, &num);
+  napi_set_named_property(env, err, "ztStatus", num);
+  napi_throw(env, err);
+  return nullptr;
+}
+
+bool get_u8(napi_env env, napi_value v, const uint8_t **p, size_t *n) {
+  bool is_ta = false;
+  napi_is_typedarray(env, v, &is_ta);
+  if (!is_ta) {
+    napi_throw_type_error(env, nullptr, "expected a Uint8Array");
+    return false;
+  }
+  napi_typedarray_type t;
+  size_t len = 0, off = 0;
+  void *data = nullptr;
+  napi_value ab;
+  napi_get_typedarray_info(env, v, &t, &len, &data, &ab, &off);
+  if (t != napi_uint8_array) {
+    napi_throw_type_error(env, nullptr, "expected a Uint8Array");
+    return false;
+  }
+  *p = static_cast<const uint8_t *>(data);
+  *n = len;
+  return true;
+}
+
+int64_t get_i64(napi_env env, napi_value v, int64_t dflt) {
+  napi_valuetype t;
+  napi_typeof(env, v, &t);
+  if (t != napi_number) return dflt;
+  int64_t x = dflt;
+  napi_get_value_int64(env, v, &x);
+  return x;
+}
+
+uint32_t get_u32(napi_env env, napi_value v, uint32_t dflt) {
+  napi_valuetype t;
+  napi_typeof(env, v, &t);
+  if (t != napi_number) return dflt;
+  uint32_t x = dflt;
+  napi_get_value_uint32(env, v, &x);
+  return x;
+}
+
+// copies a libzt-allocated result into a new Uint8Array and frees it
+napi_value new_u8(napi_env env, uint8_t *buf, size_t n) {
+  void *data = nullptr;
+  napi_value ab, ta;
+  napi_create_arraybuffer(env, n, &data, &ab);
+  if (n) memcpy(data, buf, n);
+  zt_free(buf);
+  napi_create_typedarray(env, napi_uint8_array, n, ab, 0, &ta);
+  return ta;
+}
+
+napi_value args(napi_env env, napi_callback_info info, napi_value *argv, size_t want) {
+  size_t argc = want;
+  napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr);
+  napi_value undef;
+  napi_get_undefined(env, &undef);
+  for (size_t i = argc; i < want; ++i) argv[i] = undef;
+  return undef;
+}
+
+// crc32Update(data: Uint8Array, crc: number) -> number
+napi_value crc32_update(napi_env env, napi_callback_info info) {
+  napi_value a[2];
+  args(env, info, a, 2);
+  const uint8_t *p;
+  size_t n;
+  if (!get_u8(env, a[0], &p, &n)) return nullptr;
+  uint32_t out = 0;
+  int rc = zt_crc32_update(get_u32(env, a[1], 0), p, n, &out);
+  if (rc) return throw_zt(env, rc);
+  napi_value r;
+  napi_create_uint32(env, out, &r);
+  return r;
+}
+
+// adler32Update(adler: number, data: Uint8Array) -> number
+napi_value adler32_update(napi_env env, napi_callback_info info) {
+  napi_value a[2];
+  args(env, info, a, 2);
+  const uint8_t *p;
+  size_t n;
+  if (!get_u8(env, a[1], &p, &n)) return nullptr;
+  uint32_t out = 0;
+  int rc = zt_adler32_update(get_u32(env, a[0], 1), p, n, &out);
+  if (rc) return throw_zt(env, rc);
+  napi_value r;
+  napi_create_uint32(env, out, &r);
+  return r;
+}
+
+// deflateRaw(input: Uint8Array, compressionType, lazy, level) -> Uint8Array
+napi_value deflate_raw(napi_env env, napi_callback_info info) {
+  napi_value a[4];
+  args(env, info, a, 4);
+  const uint8_t *p;
+  size_t n;
+  if (!get_u8(env, a[0], &p, &n)) return nullptr;
+  zt_deflate_opts o;
+  o.compression_type = (int)get_i64(env, a[1], 2);
+  o.lazy = (int)get_i64(env, a[2], 0);
+  o.level = (int)get_i64(env, a[3], -1);
+  uint8_t *out = nullptr;
+  size_t olen = 0;
+  int rc = zt_deflate_raw(p, n, &o, &out, &olen);
+  if (rc) return throw_zt(env, rc);
+  return new_u8(env, out, olen);
+}
+
+// inflateRaw(input: Uint8Array, index, bufferType, bufferSize, refStrict) -> {output, ip}
+napi_value inflate_raw(napi_env env, napi_callback_info info) {
+  napi_value a[5];
+  args(env, info, a, 5);
+  const uint8_t *p;
+  size_t n;
+  if (!get_u8(env, a[0], &p, &n)) return nullptr;
+  const int64_t index = get_i64(env, a[1], 0);
+  zt_inflate_opts o;
+  o.buffer_type = (int)get_i64(env, a[2], 1);
+  o.buffer_size = (size_t)get_i64(env, a[3], 0x8000);
+  bool strict = false;
+  napi_valuetype t;
+  napi_typeof(env, a[4], &t);
+  if (t == napi_boolean) napi_get_value_bool(env, a[4], &strict);
+  o.ref_strict = strict ? 1 : 0;
+  uint8_t *out = nullptr;
+  size_t olen = 0, ip = 0;
+  int rc = zt_inflate_raw(p, n, index < 0 ? 0 : (size_t)index, &o, &out, &olen, &ip);
+  if (rc) return throw_zt(env, rc);
+  napi_value obj, ipv;
+  napi_create_object(env, &obj);
+  napi_set_named_property(env, obj, "output", new_u8(env, out, olen));
+  napi_create_double(env, (double)ip, &ipv);
+  napi_set_named_property(env, obj, "ip", ipv);
+  return obj;
+}
+
+napi_value device_count(napi_env env, napi_callback_info) {
+  napi_value r;
+  napi_create_int32(env, zt_device_count(), &r);
+  return r;
+}
+
+napi_value version(napi_env env, napi_callback_info) {
+  napi_value r;
+  napi_create_string_utf8(env, zt_version(), NAPI_AUTO_LENGTH, &r);
+  return r;
+}
+
+napi_value init(napi_env env, napi_value exports) {
+  napi_property_descriptor d[] = {
+      {"crc32Update", nullptr, crc32_update, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+      {"adler32Update", nullptr, adler32_update, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+      {"deflateRaw", nullptr, deflate_raw, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+      {"inflateRaw", nullptr, inflate_raw, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+      {"deviceCount", nullptr, device_count, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+      {"version", nullptr, version, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+  };
+  napi_define_properties(env, exports, sizeof d / sizeof d[0], d);
+  return exports;
+}
+
+}  // namespace
+
+NAPI_MODULE(NODE_GYP_MODULE_NAME, init)

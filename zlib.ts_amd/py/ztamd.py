@@ -8,7 +8,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIBPATH = os.path.join(os.path.dirname(HERE), "libzt.so")
+LIBPATH = os.environ.get("ZT_LIB") or os.path.join(os.path.dirname(HERE), "libzt.so")
 
 ZT_OK = 0
 ERRORS = {
