@@ -135,12 +135,15 @@ int zt_inflate_dev(zt_inflate_plan *plan, const void *d_in, size_t n, void *d_ou
  * null stream the call returns when the data is written. */
 int zt_synth_dev(int kind, uint32_t seed, void *d_out, size_t n, void *stream);
 /* Kernel-time accounting with HIP events on the launch stream: the deflate
- * LZ77/Huffman kernel and the inflate decode kernel of the device paths. */
+ * match-finding kernel (the dominant one), the whole deflate kernel pipeline,
+ * and the inflate decode kernel of the device paths. */
 typedef struct {
-  double deflate_ms;
+  double deflate_ms; /* match_kernel */
   uint64_t deflate_launches;
-  double inflate_ms;
+  double inflate_ms; /* inflate_batch_kernel (segment decode) */
   uint64_t inflate_launches;
+  double deflate_pipeline_ms; /* match .. gather */
+  uint64_t deflate_pipelines;
 } zt_kernel_times;
 int zt_timing_enable(int on); /* resets the counters */
 int zt_timing_read(zt_kernel_times *out);

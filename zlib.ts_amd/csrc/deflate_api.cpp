@@ -49,18 +49,7 @@ struct zt_inflate_plan {
   void *jobs;
 };
 
-namespace zt {
-extern uint32_t *g_deflate_debug;
-}
-
 extern "C" {
-
-// Test hook (not part of include/zt.h): dump the first sub-chunk's per-position
-// match results and parse masks into a device buffer of >= 17000 words.
-int zt_debug_set_deflate_dump(void *d_buf) {
-  g_deflate_debug = (uint32_t *)d_buf;
-  return ZT_OK;
-}
 
 size_t zt_deflate_bound(size_t n) { return out_bound(1, n) + out_bound(0, n); }
 

@@ -28,22 +28,22 @@ int hip_fail(hipError_t e, const char *what) {
   return set_error(ZT_E_HIP, buf);
 }
 
-int timing_begin(DeviceCtx *c, hipStream_t s) {
+int timing_begin(DeviceCtx *c, hipStream_t s, int k) {
   if (!c->timing) return ZT_OK;
-  ZT_HIP(hipEventRecord(c->ev[0], s));
+  ZT_HIP(hipEventRecord(c->ev[2 * k], s));
   return ZT_OK;
 }
 
-int timing_end(DeviceCtx *c, hipStream_t s) {
+int timing_end(DeviceCtx *c, hipStream_t s, int k) {
   if (!c->timing) return ZT_OK;
-  ZT_HIP(hipEventRecord(c->ev[1], s));
+  ZT_HIP(hipEventRecord(c->ev[2 * k + 1], s));
   return ZT_OK;
 }
 
-int timing_collect(DeviceCtx *c, double *acc_ms, uint64_t *count) {
+int timing_collect(DeviceCtx *c, double *acc_ms, uint64_t *count, int k) {
   if (!c->timing) return ZT_OK;
   float ms = 0;
-  ZT_HIP(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+  ZT_HIP(hipEventElapsedTime(&ms, c->ev[2 * k], c->ev[2 * k + 1]));
   *acc_ms += ms;
   ++*count;
   return ZT_OK;
@@ -73,8 +73,7 @@ int get_ctx(DeviceCtx **out) {
     ZT_HIP(hipMalloc(&c->d_crc_x2n, sizeof x2n));
     ZT_HIP(hipMemcpy(c->d_crc_nib, nib, sizeof nib, hipMemcpyHostToDevice));
     ZT_HIP(hipMemcpy(c->d_crc_x2n, x2n, sizeof x2n, hipMemcpyHostToDevice));
-    ZT_HIP(hipEventCreate(&c->ev[0]));
-    ZT_HIP(hipEventCreate(&c->ev[1]));
+    for (auto &e : c->ev) ZT_HIP(hipEventCreate(&e));
     g_ctx[g_dev] = c;
   }
   *out = g_ctx[g_dev];

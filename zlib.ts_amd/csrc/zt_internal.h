@@ -42,16 +42,16 @@ struct DeviceCtx {
   void *h_pinned = nullptr;
   // zt_timing_enable: HIP-event kernel timing
   bool timing = false;
-  hipEvent_t ev[2] = {nullptr, nullptr};
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // [2k, 2k+1]: interval k
   zt_kernel_times times = {};
   size_t pinned_size = 0;
 };
 
-// Records ev[0] (begin) / ev[1] (end) around a launch when timing is on.
-int timing_begin(DeviceCtx *c, hipStream_t s);
-int timing_end(DeviceCtx *c, hipStream_t s);
-// After the stream is synchronized: adds the elapsed time to *acc.
-int timing_collect(DeviceCtx *c, double *acc_ms, uint64_t *count);
+// Records the begin / end event of interval k (0 or 1) when timing is on.
+int timing_begin(DeviceCtx *c, hipStream_t s, int k = 0);
+int timing_end(DeviceCtx *c, hipStream_t s, int k = 0);
+// After the stream is synchronized: adds interval k's elapsed time to *acc.
+int timing_collect(DeviceCtx *c, double *acc_ms, uint64_t *count, int k = 0);
 
 // Context of the calling thread's current device (created on first use).
 int get_ctx(DeviceCtx **out);
