@@ -141,6 +141,7 @@ def main():
     def_ms = kt["deflate_ms"] / max(1, kt["deflate_launches"])  # match_kernel (dominant deflate kernel)
     pipe_ms = kt["deflate_pipeline_ms"] / max(1, kt["deflate_pipelines"])
     inf_ms = kt["inflate_ms"] / max(1, kt["inflate_launches"])
+    tok_ms = kt["inflate_tok_ms"] / max(1, kt["inflate_toks"])
     achieved = n / (def_ms * 1e-3) / 1e9 if def_ms > 0 else 0.0
     line = {
         "metric": "GiB/s RawDeflate L6 + RawInflate on 1 GiB buffer; ratio vs ref",
@@ -162,6 +163,7 @@ def main():
         "match_kernel_ms": round(def_ms, 3),
         "deflate_pipeline_ms": round(pipe_ms, 3),
         "inflate_kernel_ms": round(inf_ms, 3),
+        "inflate_tokenize_ms": round(tok_ms, 3),
         "deflate_GiBps": round(n / (pipe_ms * 1e-3) / 2**30, 3) if pipe_ms else None,
         "inflate_GiBps": round(n / (inf_ms * 1e-3) / 2**30, 3) if inf_ms else None,
         "roofline": {"bound": "hbm", "kernel": "match_kernel", "achieved": round(achieved, 3),

@@ -140,10 +140,12 @@ int zt_synth_dev(int kind, uint32_t seed, void *d_out, size_t n, void *stream);
 typedef struct {
   double deflate_ms; /* match_kernel */
   uint64_t deflate_launches;
-  double inflate_ms; /* inflate_batch_kernel (segment decode) */
+  double inflate_ms; /* inflate decode kernels (two-phase: tokenize + resolve; else the one-wave decode) */
   uint64_t inflate_launches;
   double deflate_pipeline_ms; /* match .. gather */
   uint64_t deflate_pipelines;
+  double inflate_tok_ms; /* two-phase inflate: phase A (tokenize_kernel) alone */
+  uint64_t inflate_toks;
 } zt_kernel_times;
 int zt_timing_enable(int on); /* resets the counters */
 int zt_timing_read(zt_kernel_times *out);

@@ -170,3 +170,25 @@ def test_rank_shards_concatenate(zt, oracle):
     assert zlib.decompress(s, -15) == want
     out, ip = zt.inflate_raw(s)
     assert out == want and ip == len(s)
+
+
+def test_two_phase_inflate_is_used(zt, oracle):
+    """Our streams carry a sync point after every block: inflate decodes them
+    in two phases (tokenize units, resolve segments) and the result equals the
+    input; overlapping copies (distance < length) exercise the in-window
+    pointer jumping."""
+    parts = [oracle.gen("wordsalad", 21, (1 << 20) + 777), b"\0" * (1 << 20) + b"x",
+             b"abc" * 400000, oracle.gen("xorshift32", 22, 300001), oracle.gen("structured", 23, 1 << 20),
+             bytes(range(256)) * 3000, b"ab" * 70000 + b"q"]
+    d = b"".join(parts)
+    s = zt.deflate_raw(d)
+    zt.timing_enable(True)
+    out, ip = zt.inflate_raw(s)
+    t = zt.timing_read()
+    zt.timing_enable(False)
+    assert out == d and ip == len(s)
+    assert t["inflate_toks"] == 1, "the two-phase inflate did not run"
+    for lvl in (1, 9):
+        s = zt.deflate_raw(d, level=lvl)
+        out, ip = zt.inflate_raw(s)
+        assert out == d and ip == len(s)

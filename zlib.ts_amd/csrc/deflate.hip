@@ -713,7 +713,7 @@ __global__ __launch_bounds__(64) void block_kernel(DeflateParams P) {
   fix += 3;
   // stored: the block's bytes + 5 header bytes; Huffman forms add the
   // 3-bit marker header, padding and the 4 sync bytes
-  const uint64_t stored_bits = 8ull * (blen + 5);
+  const uint64_t stored_bits = 8ull * (blen + 10);  // + its sync point
   const uint64_t dyn_bits = ((dyn + 3 + 7) & ~7ull) + 32;
   const uint64_t fix_bits = ((fix + 3 + 7) & ~7ull) + 32;
   uint32_t bt;
@@ -844,13 +844,21 @@ __global__ __launch_bounds__(ENC_THREADS) void encode_kernel(DeflateParams P) {
   if (bt == 0) {
     // stored block: header byte, LEN, NLEN, data
     const uint8_t *raw = P.base + P.halo + (uint64_t)blk * DF_BLOCK;
+    // followed, like every block, by an empty stored block (the sync point
+    // inflate splits on), which carries BFINAL on the stream's last block
     if (t == 0) {
-      slot_bytes[0] = last ? 1 : 0;
+      slot_bytes[0] = 0;
       slot_bytes[1] = blen & 0xFF;
       slot_bytes[2] = blen >> 8;
       slot_bytes[3] = (~blen) & 0xFF;
       slot_bytes[4] = ((~blen) >> 8) & 0xFF;
-      P.slot_len[blk] = blen + 5;
+      uint8_t *e = slot_bytes + 5 + blen;
+      e[0] = last ? 1 : 0;
+      e[1] = 0;
+      e[2] = 0;
+      e[3] = 0xFF;
+      e[4] = 0xFF;
+      P.slot_len[blk] = blen + 10;
     }
     for (uint32_t i = t; i < blen; i += ENC_THREADS) slot_bytes[5 + i] = raw[i];
     return;

@@ -123,7 +123,7 @@ extern "C" {
 int zt_inflate_raw(const uint8_t *in, size_t n, size_t index, const zt_inflate_opts *opts, uint8_t **out,
                    size_t *out_len, size_t *end_ip) {
   if (!out || !out_len) return set_error(ZT_E_ARG, "null output");
-  if (!(opts && opts->ref_strict) && in && n >= index + (1u << 18)) {
+  if (!(opts && opts->ref_strict) && in && n >= index + (1u << 14)) {
     // large stream: segment-parallel decode when it carries restart points
     DeviceCtx *c;
     ZT_TRY(get_ctx(&c));

@@ -1,24 +1,30 @@
-// inflate_seg.hip -- segment-parallel inflate of one large stream.
+// inflate_seg.hip -- parallel inflate of one large stream (host orchestration).
 //
-// Our deflate starts an independent segment every 1 MiB of input (no match
-// reaches behind a segment start) and announces it with two empty stored
-// blocks, 00 00 00 FF FF 00 00 00 FF FF (deflate.hip).  Any stream carrying
-// that pattern is decoded here as follows:
-//   1. find_restarts: every position is tested for the 10-byte pattern
-//      (one 16-byte window per thread, HBM-bound), candidates are appended;
-//   2. the candidates are sorted and every candidate is decoded as a segment
-//      by its own wavefront (inflate.hip, InfJob::stops): a segment ends where
-//      a stored block ends exactly on a later candidate;
-//   3. the host follows the chain from the stream start (segment -> the
-//      candidate it stopped on -> ...), so candidates that lie inside data are
-//      never used.  A segment decoded on its own gives the stream's bytes iff
-//      none of its matches reaches behind its start -- inflate.hip reports such
-//      a match as "invalid distance" -- so any error on the chain falls back to
-//      the one-wave decode, which also yields the reference's exact error;
-//   4. the chain's outputs are compacted into the destination (64 KiB pieces).
-// Reference behaviour replaced: src/RawInflate.ts:127-143 (decompress of one
-// stream); results are identical to the sequential decode by construction.
+// This engine's deflate ends every 32 KiB block on a byte-aligned empty stored
+// block (00 00 FF FF: a *sync point* after it) and starts an independent
+// 1 MiB segment with two more (the 10-byte restart marker
+// 00 00 00 FF FF 00 00 00 FF FF; no match reaches behind it).  Streams that
+// carry sync points are decoded in two phases (inflate_tok.hip):
+//   1. find_syncs: every byte position is tested for the pattern (one 16-byte
+//      window per thread, HBM-bound); sync points are appended, flagged when
+//      the full restart marker precedes them;
+//   2. tokenize_kernel: one wave per unit (stream start, or a sync point)
+//      decodes blocks to tokens until it reaches another sync point;
+//   3. the host follows the chain from the stream start (unit -> the sync
+//      point it stopped on -> the unit starting there ...), so sync points
+//      that lie inside data are never used, and cuts the chain into segments
+//      at restart markers; output offsets are the prefix sums of the units'
+//      output lengths;
+//   4. resolve_kernel: one wave per segment writes the bytes to their final
+//      place.
+// Any error on the chain, a unit that outgrew its token slot, or a match
+// reaching behind a segment start returns 1: the caller then decodes the
+// stream with one wave (inflate.hip), which also yields the reference's
+// exact error.  Results are identical to the sequential decode by
+// construction.  Replaces src/RawInflate.ts:127-143 for such streams.
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "zt_internal.h"
@@ -27,45 +33,43 @@ namespace zt {
 
 namespace {
 
-constexpr uint32_t kMaxCand = 1u << 20;
-constexpr uint64_t kPiece = 65536;
+constexpr uint32_t kMaxSync = 1u << 22;
 
-__global__ __launch_bounds__(256) void find_restarts(const uint8_t *__restrict__ in, uint64_t lo, uint64_t n,
-                                                     uint64_t *__restrict__ list, uint32_t *__restrict__ count) {
+// ZT_INF_DEBUG=1: report why a stream left the two-phase path
+bool inf_debug() {
+  static const bool on = getenv("ZT_INF_DEBUG") != nullptr;
+  return on;
+}
+#define FALLBACK(...)                                   \
+  do {                                                  \
+    if (inf_debug()) fprintf(stderr, "[zt inflate] " __VA_ARGS__); \
+    return 1;                                           \
+  } while (0)
+constexpr uint32_t kUnitTokCap = 32768 + 64;  // a 32 KiB block has <= 32768 tokens
+
+// sync point = byte after an aligned 00 00 FF FF; list entry = pos << 1 | restart
+__global__ __launch_bounds__(256) void find_syncs(const uint8_t *__restrict__ in, uint64_t lo, uint64_t n,
+                                                  uint64_t *__restrict__ list, uint32_t *__restrict__ count) {
   const uint64_t base = (lo & ~uint64_t(15)) + ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 16;
   if (base >= n) return;
-  uint8_t b[32];
+  uint8_t b[26];
 #pragma unroll
-  for (int j = 0; j < 32; ++j) b[j] = (base + j < n) ? in[base + j] : 1;
+  for (int j = 0; j < 26; ++j) {
+    const int64_t q = (int64_t)base - 6 + j;
+    b[j] = (q >= 0 && (uint64_t)q < n) ? in[q] : 1;
+  }
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
-    const uint64_t p = base + j;
-    if (b[j + 3] == 0xFF && b[j + 4] == 0xFF && b[j + 8] == 0xFF && b[j + 9] == 0xFF && b[j] == 0 &&
-        b[j + 1] == 0 && b[j + 2] == 0 && b[j + 5] == 0 && b[j + 6] == 0 && b[j + 7] == 0 && p >= lo &&
-        p + 10 <= n) {
-      const uint32_t k = atomicAdd(count, 1u);
-      if (k < kMaxCand) list[k] = p + 10;
+    // bytes base + j .. base + j + 3 are b[j + 6 .. j + 9]
+    if (b[j + 6] == 0 && b[j + 7] == 0 && b[j + 8] == 0xFF && b[j + 9] == 0xFF) {
+      const uint64_t p = base + j + 4;
+      if (p > lo && p < n) {
+        const bool restart = b[j] == 0 && b[j + 1] == 0 && b[j + 2] == 0 && b[j + 3] == 0xFF && b[j + 4] == 0xFF &&
+                             b[j + 5] == 0 && base + j >= 6;
+        const uint32_t k = atomicAdd(count, 1u);
+        if (k < kMaxSync) list[k] = (p << 1) | (restart ? 1 : 0);
+      }
     }
-  }
-}
-
-struct Piece {
-  const uint8_t *src;
-  uint8_t *dst;
-  uint64_t len;
-};
-
-__global__ __launch_bounds__(256) void copy_pieces(const Piece *__restrict__ pieces) {
-  const Piece pc = pieces[blockIdx.x];
-  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  if (((reinterpret_cast<uintptr_t>(pc.src) | reinterpret_cast<uintptr_t>(pc.dst)) & 15) == 0) {
-    const uint64_t nv = pc.len >> 4;
-    const u32x4 *s = reinterpret_cast<const u32x4 *>(pc.src);
-    u32x4 *d = reinterpret_cast<u32x4 *>(pc.dst);
-    for (uint64_t i = threadIdx.x; i < nv; i += 256) d[i] = __builtin_nontemporal_load(&s[i]);
-    for (uint64_t i = nv * 16 + threadIdx.x; i < pc.len; i += 256) pc.dst[i] = pc.src[i];
-  } else {
-    for (uint64_t i = threadIdx.x; i < pc.len; i += 256) pc.dst[i] = pc.src[i];
   }
 }
 
@@ -75,120 +79,96 @@ size_t align256(size_t v) { return (v + 255) & ~size_t(255); }
 
 int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t index, uint8_t **d_out_io,
                          size_t out_cap, size_t *out_len, size_t *end_ip, hipStream_t s) {
-  if (n < index + (1u << 18)) return 1;  // small: one wave is as fast
-  // 1. restart candidates
+  if (n < index + (1u << 14)) return 1;  // small: one wave is as fast
+  // 1. sync points
   void *d_cand;
-  ZT_TRY(scratch(c, 5, 256 + (size_t)kMaxCand * 8, &d_cand));
+  ZT_TRY(scratch(c, 5, 256 + (size_t)kMaxSync * 8, &d_cand));
   uint32_t *d_count = static_cast<uint32_t *>(d_cand);
   uint64_t *d_list = reinterpret_cast<uint64_t *>(static_cast<uint8_t *>(d_cand) + 256);
   ZT_HIP(hipMemsetAsync(d_count, 0, 4, s));
   const uint64_t span = n - (index & ~size_t(15));
   const uint32_t grid = (uint32_t)((span + 16 * 256 - 1) / (16 * 256));
-  find_restarts<<<grid, 256, 0, s>>>(d_in, index, n, d_list, d_count);
+  ZT_TRY(timing_begin(c, s, 2));
+  find_syncs<<<grid, 256, 0, s>>>(d_in, index, n, d_list, d_count);
   ZT_HIP(hipGetLastError());
   uint32_t cnt = 0;
   ZT_HIP(hipMemcpyAsync(&cnt, d_count, 4, hipMemcpyDeviceToHost, s));
   ZT_HIP(hipStreamSynchronize(s));
-  if (cnt == 0 || cnt > kMaxCand) return 1;
-  std::vector<uint64_t> cand(cnt);
-  ZT_HIP(hipMemcpyAsync(cand.data(), d_list, (size_t)cnt * 8, hipMemcpyDeviceToHost, s));
+  if (cnt == 0 || cnt > kMaxSync) FALLBACK("%u sync points\n", cnt);
+  std::vector<uint64_t> raw(cnt);
+  ZT_HIP(hipMemcpyAsync(raw.data(), d_list, (size_t)cnt * 8, hipMemcpyDeviceToHost, s));
   ZT_HIP(hipStreamSynchronize(s));
-  std::sort(cand.begin(), cand.end());
-  cand.erase(std::unique(cand.begin(), cand.end()), cand.end());
-  cand.erase(std::remove_if(cand.begin(), cand.end(), [&](uint64_t p) { return p <= index || p >= n; }),
-             cand.end());
-  if (cand.empty()) return 1;
-  // 2. one wave per segment (candidate), outputs into per-segment scratch
-  const size_t units = cand.size() + 1;
-  std::vector<uint64_t> start(units);
-  start[0] = index;
-  for (size_t i = 1; i < units; ++i) start[i] = cand[i - 1];
-  std::vector<size_t> cap(units), off(units);
-  size_t total_cap = 0;
-  for (size_t i = 0; i < units; ++i) {
-    const uint64_t e = i + 1 < units ? start[i + 1] : n;
-    cap[i] = align256((e - start[i]) * 16 + 65536);
-    off[i] = total_cap;
-    total_cap += cap[i];
+  std::sort(raw.begin(), raw.end());
+  std::vector<uint64_t> sync;
+  std::vector<uint8_t> restart;
+  sync.reserve(raw.size());
+  restart.reserve(raw.size());
+  for (uint64_t e : raw) {
+    const uint64_t p = e >> 1;
+    if (!sync.empty() && sync.back() == p) continue;
+    sync.push_back(p);
+    restart.push_back((uint8_t)(e & 1));
   }
-  void *d_units, *d_meta;
-  ZT_TRY(scratch(c, 4, total_cap, &d_units));
-  const size_t stops_bytes = align256(cand.size() * 8);
-  const size_t jobs_bytes = align256(units * sizeof(InfJob));
-  ZT_TRY(scratch(c, 6, stops_bytes + jobs_bytes + align256(units * sizeof(InfResult)), &d_meta));
+  // 2. units: the stream start and every sync point
+  const size_t units = sync.size() + 1;
+  std::vector<TokJob> jobs(units);
+  for (size_t i = 0; i < units; ++i) {
+    TokJob &j = jobs[i];
+    j.start = i ? sync[i - 1] : index;
+    j.tok_off = (uint64_t)i * kUnitTokCap;
+    const uint64_t left = n - j.start;
+    j.tok_cap = (uint32_t)std::min<uint64_t>(kUnitTokCap, left * 8 + 64);
+    j.stop_first = (uint32_t)i;  // sync[i] is the first sync point after start
+  }
+  void *d_tok, *d_meta;
+  ZT_TRY(scratch(c, 4, units * (size_t)kUnitTokCap * 4, &d_tok));
+  const size_t stops_bytes = align256(sync.size() * 8);
+  const size_t jobs_bytes = align256(units * sizeof(TokJob));
+  const size_t res_bytes = align256(units * sizeof(TokResult));
+  ZT_TRY(scratch(c, 6, stops_bytes + jobs_bytes + res_bytes, &d_meta));
   uint64_t *d_stops = static_cast<uint64_t *>(d_meta);
-  InfJob *d_jobs = reinterpret_cast<InfJob *>(static_cast<uint8_t *>(d_meta) + stops_bytes);
-  InfResult *d_res = reinterpret_cast<InfResult *>(static_cast<uint8_t *>(d_meta) + stops_bytes + jobs_bytes);
-  std::vector<InfJob> jobs(units);
-  for (size_t i = 0; i < units; ++i) {
-    InfJob &j = jobs[i];
-    j = InfJob{};
-    j.in = d_in;
-    j.n = n;
-    j.start = start[i];
-    j.out = static_cast<uint8_t *>(d_units) + off[i];
-    j.cap = cap[i];
-    j.strict = 0;
-    j.stops = d_stops;
-    j.stop_first = (uint32_t)i;  // cand[i] is the next segment start
-    j.stop_count = cand.size();
-  }
-  ZT_HIP(hipMemcpyAsync(d_stops, cand.data(), cand.size() * 8, hipMemcpyHostToDevice, s));
-  ZT_HIP(hipMemcpyAsync(d_jobs, jobs.data(), units * sizeof(InfJob), hipMemcpyHostToDevice, s));
-  ZT_TRY(timing_begin(c, s));
-  ZT_TRY(inflate_jobs_dev(d_jobs, d_res, (int)units, s));
-  ZT_TRY(timing_end(c, s));
-  std::vector<InfResult> res(units);
-  ZT_HIP(hipMemcpyAsync(res.data(), d_res, units * sizeof(InfResult), hipMemcpyDeviceToHost, s));
+  TokJob *d_jobs = reinterpret_cast<TokJob *>(static_cast<uint8_t *>(d_meta) + stops_bytes);
+  TokResult *d_res = reinterpret_cast<TokResult *>(static_cast<uint8_t *>(d_meta) + stops_bytes + jobs_bytes);
+  ZT_HIP(hipMemcpyAsync(d_stops, sync.data(), sync.size() * 8, hipMemcpyHostToDevice, s));
+  ZT_HIP(hipMemcpyAsync(d_jobs, jobs.data(), units * sizeof(TokJob), hipMemcpyHostToDevice, s));
+  TokParams tp;
+  tp.in = d_in;
+  tp.n = n;
+  tp.stops = d_stops;
+  tp.nstops = sync.size();
+  tp.jobs = d_jobs;
+  tp.res = d_res;
+  tp.tokens = static_cast<uint32_t *>(d_tok);
+  tp.count = (uint32_t)units;
+  ZT_TRY(timing_begin(c, s, 3));
+  ZT_TRY(tokenize_units_dev(tp, s));
+  ZT_TRY(timing_end(c, s, 3));
+  std::vector<TokResult> res(units);
+  ZT_HIP(hipMemcpyAsync(res.data(), d_res, units * sizeof(TokResult), hipMemcpyDeviceToHost, s));
   ZT_HIP(hipStreamSynchronize(s));
-  ZT_TRY(timing_collect(c, &c->times.inflate_ms, &c->times.inflate_launches));
-  // 3. the chain from the stream start
-  std::vector<size_t> chain;
+  // 3. the chain from the stream start, cut into segments at restart markers
+  std::vector<ChainUnit> chain;
+  std::vector<SegJob> segs;
+  uint64_t total = 0;
   size_t u = 0;
   for (;;) {
-    const InfResult &r = res[u];
-    if (r.status != ZT_OK) return 1;  // exact error (or a match behind a false start): one wave decides
-    chain.push_back(u);
+    const TokResult &r = res[u];
+    if (r.status != ZT_OK || r.out_len > 0xFFFFFFFFull)
+      FALLBACK("unit %zu (start %llu, chain %zu): status %d detail %d ntok %u out %llu\n", u,
+               (unsigned long long)jobs[u].start, chain.size(), r.status, r.detail, r.ntok,
+               (unsigned long long)r.out_len);
+    const bool seg_start = u == 0 || restart[u - 1];
+    if (seg_start || segs.empty()) segs.push_back(SegJob{(uint32_t)chain.size(), 0});
+    chain.push_back(ChainUnit{jobs[u].tok_off, total, r.ntok, (uint32_t)r.out_len});
+    segs.back().count++;
+    total += r.out_len;
     if (r.stop_idx < 0) break;
     const size_t nx = (size_t)r.stop_idx + 1;
-    if (nx <= u || nx >= units) return 1;
+    if (nx <= u || nx >= units) FALLBACK("unit %zu: bad stop %d\n", u, r.stop_idx);
     u = nx;
   }
-  // segments that outgrew their scratch: decode again with the exact size
-  std::vector<size_t> redo;
-  for (size_t k : chain)
-    if (res[k].out_len > cap[k]) redo.push_back(k);
-  std::vector<const uint8_t *> src(units, nullptr);
-  for (size_t k : chain) src[k] = static_cast<const uint8_t *>(d_units) + off[k];
-  if (!redo.empty()) {
-    size_t tot = 0;
-    std::vector<size_t> roff(redo.size());
-    for (size_t i = 0; i < redo.size(); ++i) {
-      roff[i] = tot;
-      tot += align256(res[redo[i]].out_len);
-    }
-    void *d_redo;
-    ZT_TRY(scratch(c, 7, tot, &d_redo));
-    std::vector<InfJob> rj(redo.size());
-    for (size_t i = 0; i < redo.size(); ++i) {
-      rj[i] = jobs[redo[i]];
-      rj[i].out = static_cast<uint8_t *>(d_redo) + roff[i];
-      rj[i].cap = res[redo[i]].out_len;
-      src[redo[i]] = rj[i].out;
-    }
-    ZT_HIP(hipMemcpyAsync(d_jobs, rj.data(), rj.size() * sizeof(InfJob), hipMemcpyHostToDevice, s));
-    ZT_TRY(inflate_jobs_dev(d_jobs, d_res, (int)rj.size(), s));
-    std::vector<InfResult> rr(redo.size());
-    ZT_HIP(hipMemcpyAsync(rr.data(), d_res, rr.size() * sizeof(InfResult), hipMemcpyDeviceToHost, s));
-    ZT_HIP(hipStreamSynchronize(s));
-    for (size_t i = 0; i < redo.size(); ++i)
-      if (rr[i].status != ZT_OK || rr[i].out_len != res[redo[i]].out_len) return 1;
-  }
-  // 4. compaction
-  size_t total = 0;
-  for (size_t k : chain) total += res[k].out_len;
   *out_len = total;
-  *end_ip = res[chain.back()].end_ip;
+  *end_ip = (res[u].end_bits + 7) >> 3;
   uint8_t *d_out = *d_out_io;
   if (!d_out) {  // caller wants a library-owned buffer (scratch slot 1)
     void *p;
@@ -198,22 +178,32 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   } else if (total > out_cap) {
     return set_error(ZT_E_ARG, "output capacity too small");
   }
-  std::vector<Piece> pieces;
-  size_t pos = 0;
-  for (size_t k : chain) {
-    const size_t len = res[k].out_len;
-    for (size_t a = 0; a < len; a += kPiece)
-      pieces.push_back(Piece{src[k] + a, d_out + pos + a, std::min<uint64_t>(kPiece, len - a)});
-    pos += len;
-  }
-  if (!pieces.empty()) {
-    void *d_pieces;
-    ZT_TRY(scratch(c, 2, pieces.size() * sizeof(Piece), &d_pieces));
-    ZT_HIP(hipMemcpyAsync(d_pieces, pieces.data(), pieces.size() * sizeof(Piece), hipMemcpyHostToDevice, s));
-    copy_pieces<<<(unsigned)pieces.size(), 256, 0, s>>>(static_cast<const Piece *>(d_pieces));
-    ZT_HIP(hipGetLastError());
-  }
+  // 4. resolve, one wave per segment
+  void *d_chain;
+  const size_t chain_bytes = align256(chain.size() * sizeof(ChainUnit));
+  const size_t seg_bytes = align256(segs.size() * sizeof(SegJob));
+  ZT_TRY(scratch(c, 7, chain_bytes + seg_bytes + align256(segs.size() * 4), &d_chain));
+  ChainUnit *d_cu = static_cast<ChainUnit *>(d_chain);
+  SegJob *d_sj = reinterpret_cast<SegJob *>(static_cast<uint8_t *>(d_chain) + chain_bytes);
+  int32_t *d_st = reinterpret_cast<int32_t *>(static_cast<uint8_t *>(d_chain) + chain_bytes + seg_bytes);
+  ZT_HIP(hipMemcpyAsync(d_cu, chain.data(), chain.size() * sizeof(ChainUnit), hipMemcpyHostToDevice, s));
+  ZT_HIP(hipMemcpyAsync(d_sj, segs.data(), segs.size() * sizeof(SegJob), hipMemcpyHostToDevice, s));
+  ResolveParams rp;
+  rp.tokens = static_cast<const uint32_t *>(d_tok);
+  rp.units = d_cu;
+  rp.segs = d_sj;
+  rp.out = d_out;
+  rp.seg_status = d_st;
+  rp.nseg = (uint32_t)segs.size();
+  ZT_TRY(resolve_segments_dev(rp, s));
+  ZT_TRY(timing_end(c, s, 2));
+  std::vector<int32_t> st(segs.size());
+  ZT_HIP(hipMemcpyAsync(st.data(), d_st, segs.size() * 4, hipMemcpyDeviceToHost, s));
   ZT_HIP(hipStreamSynchronize(s));
+  ZT_TRY(timing_collect(c, &c->times.inflate_ms, &c->times.inflate_launches, 2));
+  ZT_TRY(timing_collect(c, &c->times.inflate_tok_ms, &c->times.inflate_toks, 3));
+  for (size_t i = 0; i < st.size(); ++i)
+    if (st[i] != ZT_OK) FALLBACK("segment %zu of %zu: status %d\n", i, st.size(), st[i]);
   return ZT_OK;
 }
 

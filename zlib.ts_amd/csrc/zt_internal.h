@@ -42,7 +42,7 @@ struct DeviceCtx {
   void *h_pinned = nullptr;
   // zt_timing_enable: HIP-event kernel timing
   bool timing = false;
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // [2k, 2k+1]: interval k
+  hipEvent_t ev[8] = {};  // [2k, 2k+1]: interval k (0 match, 1 deflate pipeline, 2 inflate)
   zt_kernel_times times = {};
   size_t pinned_size = 0;
 };
@@ -141,6 +141,54 @@ struct InfResult {
 // (*d_out_io null: the output goes to scratch slot 1, returned in *d_out_io)
 int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t index, uint8_t **d_out_io,
                          size_t out_cap, size_t *out_len, size_t *end_ip, hipStream_t s);
+
+
+// ---- two-phase token inflate (inflate_tok.hip) ----------------------------------
+// phase A: one unit = blocks from one sync point to the next
+struct TokJob {
+  uint64_t start;       // byte position (relative to `in`) of the unit's first block
+  uint64_t tok_off;     // first token slot
+  uint32_t tok_cap;     // token capacity
+  uint32_t stop_first;  // index of the first sync point after `start`
+};
+struct TokResult {
+  uint64_t out_len;   // bytes the unit's tokens produce
+  uint64_t end_bits;  // bit position after the unit's last block
+  uint32_t ntok;
+  int32_t status;
+  int32_t detail;
+  int32_t stop_idx;   // sync point where the unit stopped, -1 at BFINAL
+};
+struct TokParams {
+  const uint8_t *in;
+  uint64_t n;
+  const uint64_t *stops;  // sorted sync points
+  uint64_t nstops;
+  const TokJob *jobs;
+  TokResult *res;
+  uint32_t *tokens;
+  uint32_t count;
+};
+// phase B: units of the chain, grouped by segment
+struct ChainUnit {
+  uint64_t tok_off;
+  uint64_t out_off;  // absolute output offset
+  uint32_t ntok;
+  uint32_t out_len;
+};
+struct SegJob {
+  uint32_t first, count;  // chain units [first, first + count)
+};
+struct ResolveParams {
+  const uint32_t *tokens;
+  const ChainUnit *units;
+  const SegJob *segs;
+  uint8_t *out;
+  int32_t *seg_status;
+  uint32_t nseg;
+};
+int tokenize_units_dev(const TokParams &p, hipStream_t s);
+int resolve_segments_dev(const ResolveParams &p, hipStream_t s);
 
 int inflate_jobs_dev(const InfJob *d_jobs, InfResult *d_res, int count, hipStream_t s);
 int inflate_error(int status, int detail);

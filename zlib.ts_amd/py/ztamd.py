@@ -33,7 +33,8 @@ class DeflateOpts(ctypes.Structure):
 class KernelTimes(ctypes.Structure):
     _fields_ = [("deflate_ms", ctypes.c_double), ("deflate_launches", ctypes.c_uint64),
                 ("inflate_ms", ctypes.c_double), ("inflate_launches", ctypes.c_uint64),
-                ("deflate_pipeline_ms", ctypes.c_double), ("deflate_pipelines", ctypes.c_uint64)]
+                ("deflate_pipeline_ms", ctypes.c_double), ("deflate_pipelines", ctypes.c_uint64),
+                ("inflate_tok_ms", ctypes.c_double), ("inflate_toks", ctypes.c_uint64)]
 
 
 class InflateOpts(ctypes.Structure):
@@ -272,4 +273,5 @@ def timing_read():
     _check(lib.zt_timing_read(ctypes.byref(t)))
     return {"deflate_ms": t.deflate_ms, "deflate_launches": t.deflate_launches,
             "inflate_ms": t.inflate_ms, "inflate_launches": t.inflate_launches,
-            "deflate_pipeline_ms": t.deflate_pipeline_ms, "deflate_pipelines": t.deflate_pipelines}
+            "deflate_pipeline_ms": t.deflate_pipeline_ms, "deflate_pipelines": t.deflate_pipelines,
+            "inflate_tok_ms": t.inflate_tok_ms, "inflate_toks": t.inflate_toks}
