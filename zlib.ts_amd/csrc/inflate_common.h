@@ -128,7 +128,7 @@ __device__ __forceinline__ int build_table(const uint8_t *lens, int n, HuffTab *
 // cooperative 8 KiB refills (one wait per 8 KiB of input, never inside the
 // per-symbol chain); a 64-bit bit buffer in scalar registers is topped up
 // from LDS.  Positions are relative to a 16-byte aligned base below `in`.
-constexpr uint32_t IN_RING = 4096;
+constexpr uint32_t IN_RING = 8192;
 constexpr uint32_t IN_RING_WORDS = IN_RING / 4;
 constexpr uint32_t IN_HALF = IN_RING / 2;
 constexpr uint32_t IN_MASK_W = IN_RING / 4 - 1;
@@ -247,6 +247,20 @@ struct Reader {
     uint64_t want = (pos_bits_in() + maxlen + 7) >> 3;
     if (want > hi - lo) want = hi - lo;
     if (want > ip_ref) ip_ref = want;
+  }
+  // jump to bit position pb (relative to abase), reloading the ring
+  __device__ void seek_bit(uint64_t pb) {
+    const uint64_t a = pb >> 3;
+    bb = 0;
+    bc = 0;
+    ip = a;
+    fill = a & ~uint64_t(IN_HALF - 1);
+    refill_half();
+    refill_half();
+    refill();
+    const uint32_t drop = (uint32_t)(pb & 7);
+    bb >>= drop;
+    bc -= drop;
   }
   // jump to a byte position relative to `in` (stored blocks)
   __device__ void seek_byte(uint64_t p) {

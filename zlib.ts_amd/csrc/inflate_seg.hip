@@ -140,12 +140,51 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   tp.res = d_res;
   tp.tokens = static_cast<uint32_t *>(d_tok);
   tp.count = (uint32_t)units;
+  static const char *simt_env = getenv("ZT_TOK_SIMT");
+  tp.simt = simt_env ? atoi(simt_env) != 0 : 1;
+  const bool check = getenv("ZT_TOK_CHECK") != nullptr;
+  tp.dbg = nullptr;
+  if (check) {
+    void *d_dbg;
+    ZT_TRY(scratch(c, 2, units * 64 + 8 * 64 * 32, &d_dbg));
+    ZT_HIP(hipMemsetAsync(d_dbg, 0, units * 64 + 8 * 64 * 32, s));
+    tp.dbg = static_cast<uint64_t *>(d_dbg);
+  }
+  tp.dump_unit = getenv("ZT_TOK_DUMP") ? (uint32_t)atoi(getenv("ZT_TOK_DUMP")) : 0xFFFFFFFFu;
+  tp.dump_once = 0;
   ZT_TRY(timing_begin(c, s, 3));
   ZT_TRY(tokenize_units_dev(tp, s));
   ZT_TRY(timing_end(c, s, 3));
   std::vector<TokResult> res(units);
   ZT_HIP(hipMemcpyAsync(res.data(), d_res, units * sizeof(TokResult), hipMemcpyDeviceToHost, s));
   ZT_HIP(hipStreamSynchronize(s));
+  if (check) {
+    std::vector<uint64_t> dbg(units * 8);
+    ZT_HIP(hipMemcpy(dbg.data(), tp.dbg, units * 64, hipMemcpyDeviceToHost));
+    size_t bad = 0;
+    for (size_t i = 0; i < units; ++i)
+      if (dbg[i * 8]) {
+        if (bad++ < 8)
+          fprintf(stderr, "[zt tok check] unit %zu body@%llu: end simt %llu scalar %llu, tokens %llu/%llu, bytes %llu/%llu\n",
+                  i, (unsigned long long)dbg[i * 8 + 1], (unsigned long long)dbg[i * 8 + 2],
+                  (unsigned long long)dbg[i * 8 + 3], (unsigned long long)dbg[i * 8 + 4],
+                  (unsigned long long)dbg[i * 8 + 5], (unsigned long long)dbg[i * 8 + 6],
+                  (unsigned long long)dbg[i * 8 + 7]);
+      }
+    fprintf(stderr, "[zt tok check] %zu of %zu units differ\n", bad, units);
+    if (tp.dump_unit < units) {
+      std::vector<uint32_t> dd(8 * 64 * 8);
+      ZT_HIP(hipMemcpy(dd.data(), tp.dbg + units * 8, dd.size() * 4, hipMemcpyDeviceToHost));
+      for (int r = 0; r < 8; ++r) {
+        if (r > 0 && dd[(r * 64) * 8] == 0) break;
+        fprintf(stderr, "round %d R=%u last=%d\n", r, dd[(r * 64) * 8], (int)dd[(r * 64) * 8 + 6]);
+        for (int l = 0; l < 64; ++l) {
+          const uint32_t *d = &dd[(r * 64 + l) * 8];
+          fprintf(stderr, "  l%02d t=%u end=%u tok=%u e=%d fl=%u ev=%u\n", l, d[1], d[2], d[3], (int)d[4], d[5], d[7]);
+        }
+      }
+    }
+  }
   // 3. the chain from the stream start, cut into segments at restart markers
   std::vector<ChainUnit> chain;
   std::vector<SegJob> segs;

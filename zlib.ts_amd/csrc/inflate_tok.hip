@@ -30,6 +30,7 @@ namespace zt {
 
 namespace {
 
+
 struct TokShared {
   uint32_t inbuf[IN_RING_WORDS + 4];
   HuffTab lit;
@@ -140,8 +141,345 @@ __device__ __forceinline__ int tok_huffman(Reader &rd, const HuffTab *lt, const 
   }
 }
 
+
+// ------------------------------------------------ phase A, SIMT block body
+// A Huffman block body is decoded by all 64 lanes at once, in rounds of
+// 64 x SP_LANE_BITS bits, each lane from its own bit offset (speculative
+// parallel decoding of a prefix code).  Lane l starts at s_l and decodes until
+// it passes s_{l+1}, marking in a bitmap every position where a token began.
+// Decoding is deterministic, so once a lane's path meets the true token
+// sequence it *is* the true sequence.  The true start of lane l is the end of
+// lane l-1's true path; if that position is marked in lane l's bitmap, lane l
+// is synchronised and its tokens are the marks from there on (popcount).
+// DEFLATE token streams often take tens of tokens to resynchronise (extra
+// bits are raw), so unsynchronised lanes are re-decoded in parallel from
+// their true start until they merge with their old path (a marked position),
+// and the marks are corrected on the way.  A second pass decodes every lane's
+// exact range and writes its tokens at their final index.
+constexpr uint32_t SP_LANE_BITS = 960;                    // 120 bytes per lane
+constexpr uint32_t SP_WORDS = SP_LANE_BITS / 32;          // bitmap words per lane
+constexpr uint32_t SP_STAGE_BYTES = 8192;                 // staged input per round
+static_assert(64 * SP_LANE_BITS / 8 + 16 + 64 <= SP_STAGE_BYTES, "round must fit the stage");
+static_assert(SP_STAGE_BYTES <= 4 * IN_RING_WORDS, "stage lives in the reader's ring");
+
+struct SpecShared {
+  uint32_t bm[SP_WORDS][64];  // token-start bitmap, word w of lane l
+  uint32_t tail[64];          // the unit's last partial token group (staging)
+};
+
+// per-lane bit reader over the round's staged input (LDS, dword q at
+// stage[q - qbase])
+struct LaneBits {
+  const uint32_t *stage;
+  uint32_t qbase;
+  uint32_t q;      // next dword to shift in
+  uint64_t bb;
+  uint32_t bc;
+  uint32_t rel;    // bit position of bb bit 0, relative to the body start
+
+  __device__ __forceinline__ uint32_t word(uint32_t qq) const {
+    return stage[(qq - qbase) & (SP_STAGE_BYTES / 4 - 1)];
+  }
+  // abs_bit: relative to the reader's abase; rel0: the same, relative to the body
+  __device__ __forceinline__ void init(uint64_t abs_bit, uint32_t rel0) {
+    q = (uint32_t)(abs_bit >> 5);
+    const uint32_t sh = (uint32_t)abs_bit & 31;
+    bb = word(q) >> sh;
+    bc = 32 - sh;
+    ++q;
+    rel = rel0;
+  }
+  // afterwards at least 32 valid bits
+  __device__ __forceinline__ void refill() {
+    if (bc <= 32) {
+      bb |= (uint64_t)word(q) << bc;
+      bc += 32;
+      ++q;
+    }
+  }
+  __device__ __forceinline__ void consume(uint32_t n) {
+    bb >>= n;
+    bc -= n;
+    rel += n;
+  }
+};
+
+// code longer than PRI bits, per lane
+__device__ __forceinline__ int long_code_lane(const HuffTab *t, uint32_t v, uint32_t &len) {
+  const uint32_t r = __brev(v);
+  const int ml = t->maxlen;
+  for (int l = PRI + 1; l <= ml; ++l) {
+    const uint32_t c = r >> (32 - l);
+    const uint32_t k = c - t->first[l];
+    if (k < t->count[l]) {
+      len = (uint32_t)l;
+      return (int)t->sorted[t->offs[l] + k];
+    }
+  }
+  return -1;
+}
+
+// one token at the lane's position: 0 ok (tok, nbytes), 1 end of block, -1 invalid
+__device__ __forceinline__ int lane_token(LaneBits &lb, const HuffTab *lt, const HuffTab *dt, uint32_t &tok,
+                                          uint32_t &nbytes) {
+  constexpr uint32_t M = (1u << PRI) - 1;
+  lb.refill();
+  const uint32_t e = lt->pri[(uint32_t)lb.bb & M];
+  uint32_t cl, sym, ex, base;
+  if (e & 15) {
+    cl = e & 15;
+    sym = (e >> 8) & 511;
+    ex = (e >> 4) & 15;
+    base = e >> 17;
+  } else {
+    const int s = long_code_lane(lt, (uint32_t)lb.bb, cl);
+    if (s < 0) return -1;
+    sym = (uint32_t)s;
+    ex = sym > 256 ? len_extra(sym - 257) : 0;
+    base = sym > 256 ? len_base(sym - 257) : 0;
+  }
+  if (sym < 256) {
+    lb.consume(cl);
+    tok = sym;
+    nbytes = 1;
+    return 0;
+  }
+  if (sym == 256) {
+    lb.consume(cl);
+    return 1;
+  }
+  const uint32_t length = base + ((uint32_t)(lb.bb >> cl) & ((1u << ex) - 1));
+  lb.consume(cl + ex);
+  lb.refill();
+  const uint32_t d = dt->pri[(uint32_t)lb.bb & M];
+  uint32_t dcl, dsym, dex, dbase;
+  if (d & 15) {
+    dcl = d & 15;
+    dsym = (d >> 8) & 511;
+    dex = (d >> 4) & 15;
+    dbase = d >> 17;
+  } else {
+    const int s = long_code_lane(dt, (uint32_t)lb.bb, dcl);
+    if (s < 0) return -1;
+    dsym = (uint32_t)s;
+    dex = dsym < 30 ? dist_extra(dsym) : 0;
+    dbase = dsym < 30 ? dist_base(dsym) : 0;
+  }
+  if (dsym >= 30) return -1;
+  const uint32_t dist = dbase + ((uint32_t)(lb.bb >> dcl) & ((1u << dex) - 1));
+  lb.consume(dcl + dex);
+  tok = (length << 16) | dist;
+  nbytes = length;
+  return 0;
+}
+
+// lane l-1's value (lane 0: `first`), with every lane taking part (DPP wave_shr:1)
+__device__ __forceinline__ uint32_t from_prev_lane(uint32_t v, uint32_t first) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)first, (int)v, 0x138, 0xF, 0xF, false);
+}
+
+// Decode the body of a Huffman block that starts at bit `b0` (relative to
+// rd's abase) with the tables in lt / dt.  Tokens go to to.tok[to.ntok ...].
+// Returns 0 with *end_bit = the bit after the end-of-block code, 1 when the
+// body is too large for this path, or a status.
+__device__ int tok_huffman_simt(Reader &rd, uint64_t b0, const HuffTab *lt, const HuffTab *dt, TokOut &to,
+                                uint64_t &op, SpecShared *sp, uint64_t &end_bit, uint32_t *dump = nullptr) {
+  const int lane = to.lane;
+  const uint64_t lim = uni64(rd.hi) * 8 - b0;  // bits available after b0
+  if (lim >= (1ull << 31)) return 1;
+  const uint32_t limit = (uint32_t)lim;
+  uint32_t *stage = rd.inbuf;  // the reader's ring is reloaded afterwards
+  LaneBits lb;
+  lb.stage = stage;
+  uint32_t R = 0;  // true start of this round (bits from b0)
+  int dump_round = 0;
+  for (;;) {
+    // ---- stage the round's input: bytes [a0, a0 + SP_STAGE_BYTES)
+    const uint64_t a0 = ((b0 + R) >> 3) & ~uint64_t(15);
+    {
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      typedef __attribute__((address_space(1))) const u32x4 g_u32x4;
+      const uint64_t hi = uni64(rd.hi);
+#pragma unroll
+      for (uint32_t k = 0; k < SP_STAGE_BYTES / 1024; ++k) {
+        const uint64_t off = a0 + k * 1024 + (uint32_t)lane * 16;
+        u32x4 v = {0, 0, 0, 0};
+        if (off < hi) v = *(g_u32x4 *)(rd.abase + off);
+        const uint32_t w = k * 256 + (uint32_t)lane * 4;
+        stage[w] = v.x;
+        stage[w + 1] = v.y;
+        stage[w + 2] = v.z;
+        stage[w + 3] = v.w;
+      }
+      lb.qbase = (uint32_t)(a0 >> 2);
+    }
+    for (uint32_t w = 0; w < SP_WORDS; ++w) sp->bm[w][lane] = 0;
+    wave_sync();
+    // ---- pass 1: lane l from s_l past s_{l+1}, marking token starts
+    const uint32_t s_l = R + (uint32_t)lane * SP_LANE_BITS;
+    const uint32_t s_next = s_l + SP_LANE_BITS;
+    const bool in_range = s_l < limit;
+    uint32_t end = s_l, ev_pos = 0;  // ev_pos: start of the EOB / invalid token
+    int flags = 0;                   // 1 end of block, 2 invalid
+    bool todo = in_range;
+    uint32_t from = s_l;             // where this lane's current decode starts
+    bool repair = false;
+    for (int iter = 0;; ++iter) {
+      if (iter > 66) return ZT_E_INPUT_BROKEN;
+      bool active = todo;
+      uint32_t cw = 0, cwi = 0;  // bitmap word being assembled, its index
+      uint32_t merge = 0xFFFFFFFFu;
+      if (active) {
+        lb.init(b0 + from, from);
+        cwi = (from - s_l) >> 5;
+        cw = 0;
+        if (!repair) flags = 0;
+        // marks below a repair's start are off every path it can merge with
+        for (uint32_t x = 0; x < cwi; ++x) sp->bm[x][lane] = 0;
+      }
+      while (__ballot(active)) {
+        if (active) {
+          const uint32_t p = lb.rel - s_l;  // < SP_LANE_BITS while decoding this lane's range
+          const uint32_t wi = p >> 5;
+          if (wi != cwi) {
+            // leave word cwi: new marks below, on a repair old marks are stale
+            sp->bm[cwi][lane] = cw;
+            for (uint32_t x = cwi + 1; x < wi; ++x) sp->bm[x][lane] = 0;
+            cwi = wi;
+            cw = 0;
+          }
+          if (repair && ((sp->bm[wi][lane] >> (p & 31)) & 1)) {
+            // merged with the old path: the old marks from p on are right
+            merge = p;
+            const uint32_t below = (p & 31) ? (0xFFFFFFFFu >> (32 - (p & 31))) : 0u;
+            sp->bm[wi][lane] = (cw & below) | (sp->bm[wi][lane] & ~below);
+            active = false;
+          } else {
+            cw |= 1u << (p & 31);
+            uint32_t tk, nb;
+            const int r = lane_token(lb, lt, dt, tk, nb);
+            if (r != 0 || lb.rel > limit) {
+              flags = r > 0 ? 1 : 2;
+              ev_pos = lb.rel - 0;  // provisional; fixed below
+              ev_pos = s_l + p;
+              end = lb.rel;
+              active = false;
+            } else if (lb.rel >= s_next) {
+              end = lb.rel;
+              flags = 0;
+              active = false;
+            }
+            if (!active) {
+              sp->bm[cwi][lane] = cw;
+              for (uint32_t x = cwi + 1; x < SP_WORDS; ++x) sp->bm[x][lane] = 0;
+            }
+          }
+        }
+      }
+      wave_sync();
+      // ---- which lanes are on the true path?
+      const uint32_t t = from_prev_lane(end, R);
+      const uint32_t tp = t - s_l;
+      const bool synced = in_range && t >= s_l && tp < SP_LANE_BITS && ((sp->bm[tp >> 5][lane] >> (tp & 31)) & 1);
+      const uint64_t U = __ballot(!synced);
+      const uint64_t E = __ballot(synced && flags != 0 && ev_pos >= t);
+      const int f = U ? __builtin_ctzll(U) : 64;
+      const int e = E ? __builtin_ctzll(E) : 64;
+      if (e < f) {
+        // the block ends (or breaks) in lane e
+        if (__builtin_amdgcn_readlane(flags, e) == 2) return ZT_E_INVALID_SYMBOL;
+        break;
+      }
+      if (f == 64) break;  // every lane synchronised, the block continues
+      if (!__builtin_amdgcn_readlane((int)in_range, f)) return ZT_E_INPUT_BROKEN;  // runs past the input
+      // re-decode every unsynchronised lane from its (current) true start
+      // (a lane whose predecessor stopped short of it waits: that predecessor
+      // is off the true path and is repaired first)
+      todo = in_range && !synced && t >= s_l && tp < SP_LANE_BITS;
+      if (todo) from = t;
+      repair = true;
+      (void)merge;
+    }
+    // final per-lane state: true start t, tokens = marks in [t, ev or end)
+    const uint32_t t = from_prev_lane(end, R);
+    const uint64_t E = __ballot(flags != 0 && ev_pos >= t && in_range);
+    const int e = E ? __builtin_ctzll(E) : 64;
+    const int last = e < 64 ? e : 63;
+    const bool eob = e < 64;
+    const bool use = lane <= last;
+    uint32_t my_tok = 0;
+    if (use) {
+      const uint32_t lo = t - s_l;
+      const uint32_t hi_p = (lane == e) ? ev_pos - s_l : SP_LANE_BITS;  // marks at p < hi_p
+      for (uint32_t w = lo >> 5; w < SP_WORDS && w * 32 < hi_p; ++w) {
+        uint32_t m = sp->bm[w][lane];
+        if (w == (lo >> 5)) m &= 0xFFFFFFFFu << (lo & 31);
+        if (hi_p < (w + 1) * 32) m &= (hi_p & 31) ? (0xFFFFFFFFu >> (32 - (hi_p & 31))) : 0u;
+        my_tok += __popc(m);
+      }
+    }
+    if (dump && dump_round < 8) {
+      uint32_t *d = dump + (dump_round * 64 + lane) * 8;
+      d[0] = R;
+      d[1] = t;
+      d[2] = end;
+      d[3] = my_tok;
+      d[4] = (uint32_t)e;
+      d[5] = (uint32_t)flags;
+      d[6] = (uint32_t)last;
+      d[7] = ev_pos;
+      ++dump_round;
+    }
+    uint32_t tok_incl = my_tok;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t a = __shfl_up(tok_incl, off, 64);
+      if (lane >= off) tok_incl += a;
+    }
+    const uint32_t tot_tok = __builtin_amdgcn_readlane(tok_incl, last);
+    const uint32_t nt0 = uni(to.ntok);
+    if ((uint64_t)nt0 + tot_tok > to.cap) return ZT_E_NOMEM;
+    const uint32_t r_end = eob ? __builtin_amdgcn_readlane(end, e) : __builtin_amdgcn_readlane(end, 63);
+    // ---- pass 2: exact ranges, tokens written at their index
+    const uint32_t nt1 = nt0 + tot_tok;
+    const uint32_t tail_base = nt1 & ~63u;
+    to.flush_partial();
+    sp->tail[lane] = to.stg;
+    wave_sync();
+    uint32_t idx = nt0 + tok_incl - my_tok;
+    const uint32_t idx_end = idx + my_tok;
+    uint32_t my_by = 0;
+    bool active = use && my_tok > 0;
+    if (active) lb.init(b0 + t, t);
+    uint32_t *tokp = to.tok;
+    while (__ballot(active)) {
+      if (active) {
+        uint32_t tk = 0, nb = 0;
+        lane_token(lb, lt, dt, tk, nb);
+        tokp[idx] = tk;
+        my_by += nb;
+        if (idx >= tail_base) sp->tail[idx & 63] = tk;
+        if (++idx >= idx_end) active = false;
+      }
+    }
+    wave_sync();
+    uint32_t by = my_by;
+#pragma unroll
+    for (int off = 32; off; off >>= 1) by += __shfl_xor(by, off, 64);
+    to.ntok = nt1;
+    to.stg = sp->tail[lane];
+    op += uni(by);
+    if (eob) {
+      end_bit = b0 + r_end;
+      return ZT_OK;
+    }
+    R = r_end;
+  }
+}
+
 __global__ __launch_bounds__(64) void tokenize_kernel(TokParams P) {
   __shared__ TokShared sh;
+  __shared__ SpecShared spsh;
   const uint32_t u = blockIdx.x;
   const int lane = threadIdx.x & 63;
   const TokJob job = P.jobs[u];
@@ -198,7 +536,46 @@ __global__ __launch_bounds__(64) void tokenize_kernel(TokParams P) {
     } else {
       status = read_tables<false>(rd, sh.lens, &sh.lit, &sh.dist, btype, lane, detail);
       if (status) break;
-      status = tok_huffman(rd, &sh.lit, &sh.dist, to, op);
+      uint64_t end_bit = 0;
+      const uint64_t body0 = rd.pos_bits();
+      const uint32_t nt_before = uni(to.ntok);
+      const uint64_t op_before = op;
+      uint32_t *dump = (P.dbg && u == P.dump_unit && P.dump_once == 0) ? reinterpret_cast<uint32_t *>(P.dbg + (uint64_t)P.count * 8) : nullptr;
+      int r = P.simt ? tok_huffman_simt(rd, body0, &sh.lit, &sh.dist, to, op, &spsh, end_bit, dump) : 1;
+      if (P.dbg && r == 0) {
+        // shadow check: decode the same body with one lane and compare
+        const uint64_t s_end = end_bit, s_op = op;
+        const uint32_t s_nt = uni(to.ntok);
+        rd.seek_bit(body0);
+        to.ntok = nt_before;
+        to.stg = 0;
+        op = op_before;
+        r = tok_huffman(rd, &sh.lit, &sh.dist, to, op);
+        const uint64_t c_end = rd.pos_bits();
+        if (lane == 0 && (c_end != s_end || uni(to.ntok) != s_nt || op != s_op)) {
+          uint64_t *d = P.dbg + (uint64_t)u * 8;
+          if (d[0] == 0) {
+            d[0] = 1;
+            d[1] = body0;
+            d[2] = s_end;
+            d[3] = c_end;
+            d[4] = s_nt - nt_before;
+            d[5] = uni(to.ntok) - nt_before;
+            d[6] = s_op - op_before;
+            d[7] = op - op_before;
+          }
+        }
+        if (r == 0) r = 2;  // already decoded (position is current)
+      }
+      if (r == 2) {
+        r = 0;
+      } else if (r == 1) {
+        status = tok_huffman(rd, &sh.lit, &sh.dist, to, op);
+      } else if (r == 0) {
+        rd.seek_bit(end_bit);
+      } else {
+        status = r;
+      }
       if (status) break;
     }
     if (!bfinal) {

@@ -168,6 +168,10 @@ struct TokParams {
   TokResult *res;
   uint32_t *tokens;
   uint32_t count;
+  int simt;           // 0: one-lane (scalar) body decode only
+  uint64_t *dbg;      // debug: per unit 8 words comparing the SIMT and scalar body decodes, or null
+  uint32_t dump_unit; // debug: unit whose first SIMT block dumps per-round lane state after dbg[count * 8]
+  uint32_t dump_once;
 };
 // phase B: units of the chain, grouped by segment
 struct ChainUnit {
