@@ -121,7 +121,7 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
     j.stop_first = (uint32_t)i;  // sync[i] is the first sync point after start
   }
   void *d_tok, *d_meta;
-  ZT_TRY(scratch(c, 4, units * (size_t)kUnitTokCap * 4, &d_tok));
+  ZT_TRY(scratch(c, 4, (units * (size_t)kUnitTokCap + 256) * 4, &d_tok));  // + slack: chunked token reads
   const size_t stops_bytes = align256(sync.size() * 8);
   const size_t jobs_bytes = align256(units * sizeof(TokJob));
   const size_t res_bytes = align256(units * sizeof(TokResult));

@@ -609,21 +609,41 @@ __device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t src_lane) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src_lane << 2), (int)v);
 }
 
-__device__ __forceinline__ uint32_t incl_scan(uint32_t x, int lane) {
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t y = __shfl_up(x, off, 64);
-    if (lane >= off) x += y;
-  }
+// inclusive prefix sum over the wave (DPP row shifts + row broadcasts)
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false); // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false); // row_bcast:31
   return x;
 }
 
+__device__ __forceinline__ uint32_t tok_len(uint32_t t) { return (t >> 16) ? (t >> 16) : 1u; }
+
+constexpr uint32_t RS_TOK_RING = 1024;        // tokens staged in LDS (16 chunks of 64)
+constexpr uint32_t RS_AHEAD = 12;             // chunks in flight ahead of the cursor
+constexpr uint32_t RS_FLUSH = 8192;           // output flush granule
+
 struct ResolveShared {
-  uint8_t ring[RING];
+  uint8_t ring[RING];          // 32 KiB history, also the output staging
+  uint32_t tok[RS_TOK_RING];   // token chunks, filled by LDS-DMA
   uint32_t mark[64];
 };
 
-__device__ __forceinline__ uint32_t tok_len(uint32_t t) { return (t >> 16) ? (t >> 16) : 1u; }
+typedef unsigned int u32x4r __attribute__((ext_vector_type(4)));
+
+// ring bytes [lo, hi) (segment positions) to out + lo (out 16-aligned when possible)
+__device__ __forceinline__ void rs_flush(const ResolveShared *sh, uint8_t *out, uint64_t lo, uint64_t hi, int lane) {
+  if (lo >= hi) return;
+  if ((((uintptr_t)out + lo) & 15) == 0 && ((hi - lo) & 15) == 0) {
+    for (uint64_t p = lo + (uint64_t)lane * 16; p < hi; p += 1024)
+      *reinterpret_cast<u32x4r *>(out + p) = *reinterpret_cast<const u32x4r *>(&sh->ring[p & RING_MASK]);
+  } else {
+    for (uint64_t p = lo + lane; p < hi; p += 64) out[p] = sh->ring[p & RING_MASK];
+  }
+}
 
 __global__ __launch_bounds__(64) void resolve_kernel(ResolveParams P) {
   __shared__ ResolveShared sh;
@@ -634,29 +654,37 @@ __global__ __launch_bounds__(64) void resolve_kernel(ResolveParams P) {
   uint8_t *out = P.out + seg_out;
   sh.mark[lane] = 0;
   uint32_t seq = 0;
-  uint64_t op = 0;  // segment-relative output position
+  uint64_t op = 0;       // segment-relative output position
+  uint64_t flushed = 0;  // bytes [0, flushed) are in HBM
   int status = ZT_OK;
   for (uint32_t k = 0; k < sj.count && status == ZT_OK; ++k) {
     const ChainUnit cu = P.units[sj.first + k];
     const uint32_t *tk = P.tokens + cu.tok_off;
     const uint32_t ntok = cu.ntok;
-    // tokens [base, base + 256) live in A, B, C, D (lane i: token base + 64 r + i)
-    uint32_t base = 0;
-    uint32_t A = (uint32_t)lane < ntok ? tk[lane] : 0u;
-    uint32_t B = 64u + lane < ntok ? tk[64 + lane] : 0u;
-    uint32_t C = 128u + lane < ntok ? tk[128 + lane] : 0u;
-    uint32_t D = 192u + lane < ntok ? tk[192 + lane] : 0u;
+    const uint32_t nchunks = (ntok + 63) / 64;
+    uint32_t issued = 0;  // token chunks requested for this unit
     uint32_t cur = 0, rem = 0;
     const uint64_t op_unit = op;
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // nothing of the previous unit in flight
     while (cur < ntok) {
-      const uint32_t c = cur - base;  // 0..63
-      const uint32_t si = c + (uint32_t)lane;
-      const uint32_t ta = bperm(A, si & 63), tb = bperm(B, si & 63);
-      const bool valid = cur + (uint32_t)lane < ntok;
-      const uint32_t t = si < 64 ? ta : tb;
+      // ---- tokens [cur, cur + 64) must be in LDS: chunks < need landed
+      const uint32_t need = (cur >> 6) + 2 < nchunks ? (cur >> 6) + 2 : nchunks;
+      const uint32_t want = need + RS_AHEAD < nchunks ? need + RS_AHEAD : nchunks;
+      while (issued < want) {
+        __builtin_amdgcn_global_load_lds(tk + (uint64_t)issued * 64 + lane,
+                                         &sh.tok[(issued * 64) & (RS_TOK_RING - 1)], 4, 0, 0);
+        ++issued;
+      }
+      if (issued - need >= RS_AHEAD)
+        __builtin_amdgcn_s_waitcnt(0x0F70 | RS_AHEAD);  // vmcnt(RS_AHEAD)
+      else
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+      const uint32_t ti = cur + (uint32_t)lane;
+      const bool valid = ti < ntok;
+      const uint32_t t = sh.tok[ti & (RS_TOK_RING - 1)];
       const uint32_t len = valid ? tok_len(t) : 0u;
-      const uint32_t S = incl_scan(len, lane);
-      const uint32_t total = uni(__builtin_amdgcn_readlane(S, 63)) - rem;
+      const uint32_t S = wave_incl_scan(len);
+      const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)S, 63) - rem;
       const uint32_t W = total < 64 ? total : 64;
       // token i + 1 starts at S_i - rem inside the window
       ++seq;
@@ -664,25 +692,28 @@ __global__ __launch_bounds__(64) void resolve_kernel(ResolveParams P) {
       if (valid && p > 0 && p < 64) sh.mark[p] = seq;
       wave_sync();
       const uint64_t starts = __ballot(sh.mark[lane] == seq);
-      const uint32_t ti = __popcll(starts & (~0ull >> (63 - lane)));  // token of byte `lane`
-      const uint32_t tj = bperm(t, ti);
+      const uint32_t owner = __popcll(starts & (~0ull >> (63 - lane)));  // token of byte `lane`
+      const uint32_t tj = bperm(t, owner);
+      const uint32_t sj_ = bperm(S - len, owner);  // its start (before rem)
       uint32_t val = 0;
-      bool bad = false;
       int32_t ptr = -1;
+      bool bad = false;
       if ((uint32_t)lane < W) {
         if ((tj >> 16) == 0) {
           val = tj & 0xFF;
         } else {
           const uint32_t dist = tj & 0xFFFF;
-          const uint64_t pos = op + (uint64_t)lane;
-          if (dist > pos) {
+          // byte k of a match is history[start - dist + k mod dist]: it depends
+          // only on bytes before the match
+          const uint64_t tstart = op + (uint64_t)lane - ((uint64_t)rem + lane - sj_);
+          const uint32_t kk = rem + (uint32_t)lane - sj_;
+          const uint64_t src = tstart - dist + (kk < dist ? kk : kk % dist);
+          if (dist > tstart) {
             bad = true;  // reaches behind the segment start
+          } else if (src >= op) {
+            ptr = (int32_t)(src - op);
           } else {
-            const uint64_t src = pos - dist;
-            if (src >= op)
-              ptr = (int32_t)(src - op);
-            else
-              val = sh.ring[src & RING_MASK];
+            val = sh.ring[src & RING_MASK];
           }
         }
       }
@@ -704,29 +735,26 @@ __global__ __launch_bounds__(64) void resolve_kernel(ResolveParams P) {
           }
         }
       }
-      if ((uint32_t)lane < W) {
-        sh.ring[(op + lane) & RING_MASK] = (uint8_t)val;
-        out[op + lane] = (uint8_t)val;
-      }
+      if ((uint32_t)lane < W) sh.ring[(op + lane) & RING_MASK] = (uint8_t)val;
       wave_sync();
       op += W;
+      if (op - flushed >= RS_FLUSH) {
+        const uint64_t upto = flushed + RS_FLUSH;
+        rs_flush(&sh, out, flushed, upto, lane);
+        flushed = upto;
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // keep vmcnt counting token chunks only
+      }
       // advance past the tokens that end inside this window
       const uint64_t done = __ballot(valid && S <= rem + W);
-      const uint32_t kk = (uint32_t)__popcll(done);
-      const uint32_t s_last = kk ? uni(__builtin_amdgcn_readlane(S, kk - 1)) : 0u;
+      const uint32_t kdone = (uint32_t)__popcll(done);
+      const uint32_t s_last = kdone ? (uint32_t)__builtin_amdgcn_readlane((int)S, kdone - 1) : 0u;
       rem = rem + W - s_last;
-      cur += kk;
-      while (cur - base >= 64) {
-        A = B;
-        B = C;
-        C = D;
-        base += 64;
-        const uint32_t ix = base + 192 + (uint32_t)lane;
-        D = ix < ntok ? tk[ix] : 0u;
-      }
+      cur += kdone;
     }
     if (op - op_unit != cu.out_len) status = ZT_E_INPUT_BROKEN;
   }
+  wave_sync();
+  if (status == ZT_OK) rs_flush(&sh, out, flushed, op, lane);
   if (lane == 0) P.seg_status[sg] = status;
 }
 
