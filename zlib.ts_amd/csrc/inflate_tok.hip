@@ -285,9 +285,11 @@ __device__ __forceinline__ uint32_t from_prev_lane(uint32_t v, uint32_t first) {
 __device__ int tok_huffman_simt(Reader &rd, uint64_t b0, const HuffTab *lt, const HuffTab *dt, TokOut &to,
                                 uint64_t &op, SpecShared *sp, uint64_t &end_bit, uint32_t *dump = nullptr) {
   const int lane = to.lane;
-  const uint64_t lim = uni64(rd.hi) * 8 - b0;  // bits available after b0
-  if (lim >= (1ull << 31)) return 1;
-  const uint32_t limit = (uint32_t)lim;
+  // bits available after b0 (positions are u32: a body past 2^31 bits -- a
+  // 256 MiB single block -- runs into the limit and is reported as broken,
+  // which sends the stream to the one-wave decoder)
+  const uint64_t lim = uni64(rd.hi) * 8 - b0;
+  const uint32_t limit = lim < 0x7FFFFFFFull ? (uint32_t)lim : 0x7FFFFFFFu;
   uint32_t *stage = rd.inbuf;  // the reader's ring is reloaded afterwards
   LaneBits lb;
   lb.stage = stage;
