@@ -40,11 +40,14 @@ namespace zt {
 
 constexpr int DF_BLOCK = 32768;
 constexpr int DF_SUB = 4096;
-constexpr int DF_RING = DF_BLOCK + DF_SUB;  // 36864 = 9 * 4096
+constexpr int DF_RING = 32768;  // power of two: ring index = rel & (DF_RING - 1)
 constexpr int DF_SLOT = DF_BLOCK + DF_BLOCK / 8 + 1024;  // per-block slot: fits a forced fixed-code block
 constexpr int DF_HBITS = 13;
 constexpr int DF_THREADS = 1024;
-constexpr int DF_MAXDIST = 32768;
+// the ring holds [p1 - DF_RING, p1) while sub-chunk [p0, p1) is searched;
+// a super-chunk loads DF_HIST bytes of history first (whole sub-chunks)
+constexpr int DF_HIST = DF_RING - DF_SUB;     // 28672
+constexpr int DF_MAXDIST = DF_HIST - 64;      // 28608
 constexpr int ENC_THREADS = 256;
 // Independent segments of 1 MiB: restart points for segment-parallel inflate
 constexpr uint32_t kRestartBlocks = 32;
@@ -64,6 +67,7 @@ struct DeflateParams {
   int nice_len;
   int lazy;
   int too_far;
+  int good;             // a carried match this long cuts the chain walk to a quarter
   int skip_len;         // a carried match at least this long is taken without a search
   int klen;             // chain key length: 3, 4, 6 or 8 bytes (shorter matches come from near probes)
   int probe;            // near distances 1..probe checked for matches shorter than klen
@@ -122,10 +126,7 @@ struct MatchShared {
   uint16_t hbuf[DF_SUB + 64];       // hashes of the positions being linked
 };
 
-__device__ __forceinline__ uint32_t ridx(uint32_t rel) {
-  uint32_t q = __umulhi(rel >> 12, 0x1C71C71Du);  // (rel >> 12) / 9, exact for rel < 2^31
-  return rel - q * (uint32_t)DF_RING;
-}
+__device__ __forceinline__ uint32_t ridx(uint32_t rel) { return rel & (DF_RING - 1); }
 __device__ __forceinline__ uint32_t ld8(const MatchShared *s, uint32_t rel) {
   return reinterpret_cast<const uint8_t *>(s->ring)[ridx(rel)];
 }
@@ -207,87 +208,126 @@ __device__ void chain_build(MatchShared *s, uint32_t lo, uint32_t hi, Key key) {
   __syncthreads();
 }
 
+// 4 bytes at byte x of a register window (x a compile-time constant after unrolling)
+template <int X>
+__device__ __forceinline__ uint32_t win32(const uint32_t (&w)[8]) {
+  return (X & 3) ? __builtin_amdgcn_alignbyte(w[(X >> 2) + 1], w[X >> 2], X & 3) : w[X >> 2];
+}
+
+constexpr int DF_NEAR = 16;  // near distances probed from registers
+
+// matches shorter than the chain key at distances 1..probe, from a register
+// window of bytes [pb - 16, pb + 16): longest wins, ties to the nearest
+template <int K, int D>
+__device__ __forceinline__ void near_probe(const uint32_t (&w)[8], uint32_t cur0, uint32_t cur1, uint32_t p,
+                                           uint32_t max_len, int probe, uint32_t &best_len, uint32_t &best_dist) {
+  if constexpr (D <= DF_NEAR) {
+    if (D <= probe && (uint32_t)D <= p) {
+      const uint32_t m0 = win32<16 + K - D>(w) ^ cur0;
+      if ((m0 & 0xFFFFFFu) == 0) {
+        uint32_t len;
+        if (m0) {
+          len = 3;
+        } else {
+          const uint32_t m1 = win32<20 + K - D>(w) ^ cur1;
+          len = m1 ? 4 + ((uint32_t)(__ffs(m1) - 1) >> 3) : 8;
+        }
+        if (len > max_len) len = max_len;
+        if (len > best_len) {
+          best_len = len;
+          best_dist = D;
+        }
+      }
+    }
+    near_probe<K, D + 1>(w, cur0, cur1, p, max_len, probe, best_len, best_dist);
+  }
+}
+
+// longest match for position pb + K (carry: the previous position's match)
+template <int K>
+__device__ __forceinline__ uint32_t search_pos(const MatchShared *s, const DeflateParams &P, const uint32_t (&w)[8],
+                                               uint32_t pb, uint32_t p1, Key key, uint32_t &carry_len,
+                                               uint32_t &carry_dist) {
+  const uint32_t p = pb + K;
+  if (p >= p1) return 0;
+  const uint32_t klen = (uint32_t)P.klen;
+  const uint32_t max_len = (p1 - p) < 258 ? (p1 - p) : 258;
+  uint32_t best_len = 0, best_dist = 0;
+  if (max_len >= 3) {
+    if (carry_len > 3) {
+      best_len = carry_len - 1;
+      best_dist = carry_dist;
+    }
+    const uint32_t cur = win32<16 + K>(w);
+    const uint32_t cur2 = win32<20 + K>(w);
+    if ((int)best_len < P.skip_len && max_len >= klen) {
+      // a good carried match needs only a short look for a better one
+      const int max_hops = (int)best_len >= P.good ? (P.max_chain >> 2) : P.max_chain;
+      // the word ending at best_len: a candidate can only win if it matches there
+      uint32_t o = best_len >= 4 ? best_len - 3 : 0;
+      uint32_t pw = best_len >= 4 ? ld32(s, p + o) : 0u;
+      uint32_t link = s->prev[ridx(p)];
+      uint32_t q = p;
+      int hops = 0;
+#pragma unroll 1
+      while (link && hops < max_hops) {
+        q -= link;
+        if (p - q > DF_MAXDIST) break;
+        ++hops;
+        link = s->prev[ridx(q)];
+        if (best_len >= 4 && ld32(s, q + o) != pw) continue;
+        if (((ld32(s, q) ^ cur) & key.kmask) != 0) continue;
+        if (key.kmask2 && ((ld32(s, q + 4) ^ cur2) & key.kmask2) != 0) continue;
+        uint32_t len = klen;
+        while (len < max_len) {
+          uint32_t x = ld32(s, q + len) ^ ld32(s, p + len);
+          if (x) {
+            len += (uint32_t)(__ffs(x) - 1) >> 3;
+            break;
+          }
+          len += 4;
+        }
+        if (len > max_len) len = max_len;
+        if (len > best_len) {
+          best_len = len;
+          best_dist = p - q;
+          if ((int)len >= P.nice_len || len >= max_len) break;
+          o = len - 3;
+          pw = ld32(s, p + o);
+        }
+      }
+    }
+    if (best_len < klen) near_probe<K, 1>(w, cur, cur2, p, max_len, P.probe, best_len, best_dist);
+  }
+  carry_len = best_len;
+  carry_dist = best_dist;
+  if (best_len == 3 && best_dist > (uint32_t)P.too_far) best_len = 0;
+  return best_len >= 3 ? (best_len << 16) | best_dist : 0u;
+}
+
 // longest match for positions [p0, p1) (4 per thread) -> res_out[p - p0]
 __device__ void search_sub(const MatchShared *s, const DeflateParams &P, uint32_t p0, uint32_t p1, Key key,
                            uint32_t *res_out) {
   const uint32_t t = threadIdx.x;
-  const uint32_t klen = (uint32_t)P.klen;
-  uint32_t carry_len = 0, carry_dist = 0;
-  uint32_t out[4] = {0, 0, 0, 0};
+  const uint32_t pb = p0 + t * 4;
+  if (pb >= p1) return;
+  // bytes [pb - 16, pb + 16) (pb is a multiple of 4; before rel 0 the words
+  // are never used: near distances stay <= p)
+  uint32_t w[8];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const uint32_t p = p0 + t * 4 + k;
-    if (p >= p1) break;
-    const uint32_t max_len = (p1 - p) < 258 ? (p1 - p) : 258;
-    uint32_t best_len = 0, best_dist = 0;
-    if (max_len >= 3) {
-      if (carry_len > 3) {
-        best_len = carry_len - 1;
-        best_dist = carry_dist;
-      }
-      const uint32_t cur = ld32(s, p);
-      const uint32_t cur2 = key.kmask2 ? ld32(s, p + 4) : 0u;
-      if ((int)best_len < P.skip_len && max_len >= klen) {
-        // the word ending at best_len: a candidate can only win if it matches there
-        uint32_t o = best_len >= 4 ? best_len - 3 : 0;
-        uint32_t pw = best_len >= 4 ? ld32(s, p + o) : 0u;
-        uint32_t link = s->prev[ridx(p)];
-        uint32_t q = p;
-        int hops = 0;
-#pragma unroll 1
-        while (link && hops < P.max_chain) {
-          q -= link;
-          if (p - q > DF_MAXDIST) break;
-          ++hops;
-          link = s->prev[ridx(q)];
-          if (best_len >= 4 && ld32(s, q + o) != pw) continue;
-          if (((ld32(s, q) ^ cur) & key.kmask) != 0) continue;
-          if (key.kmask2 && ((ld32(s, q + 4) ^ cur2) & key.kmask2) != 0) continue;
-          uint32_t len = klen;
-          while (len < max_len) {
-            uint32_t x = ld32(s, q + len) ^ ld32(s, p + len);
-            if (x) {
-              len += (uint32_t)(__ffs(x) - 1) >> 3;
-              break;
-            }
-            len += 4;
-          }
-          if (len > max_len) len = max_len;
-          if (len > best_len) {
-            best_len = len;
-            best_dist = p - q;
-            if ((int)len >= P.nice_len || len >= max_len) break;
-            o = len - 3;
-            pw = ld32(s, p + o);
-          }
-        }
-      }
-      if (best_len < klen) {
-        // matches shorter than the chain key at near distances
-        for (int d = 1; d <= P.probe && (uint32_t)d <= p; ++d) {
-          if (((ld32(s, p - d) ^ cur) & 0xFFFFFFu) == 0) {
-            uint32_t len = 3;
-            while (len < max_len && ld8(s, p - d + len) == ld8(s, p + len)) ++len;
-            if (len > best_len) {
-              best_len = len;
-              best_dist = d;
-            }
-          }
-        }
-      }
-    }
-    carry_len = best_len;
-    carry_dist = best_dist;
-    if (best_len == 3 && best_dist > (uint32_t)P.too_far) best_len = 0;
-    out[k] = best_len >= 3 ? (best_len << 16) | best_dist : 0u;
-  }
-  const uint32_t p = p0 + t * 4;
-  if (p + 4 <= p1) {
+  for (int i = 0; i < 8; ++i) w[i] = s->ring[ridx(pb - 16 + 4 * i) >> 2];
+  uint32_t carry_len = 0, carry_dist = 0;
+  uint32_t out[4];
+  out[0] = search_pos<0>(s, P, w, pb, p1, key, carry_len, carry_dist);
+  out[1] = search_pos<1>(s, P, w, pb, p1, key, carry_len, carry_dist);
+  out[2] = search_pos<2>(s, P, w, pb, p1, key, carry_len, carry_dist);
+  out[3] = search_pos<3>(s, P, w, pb, p1, key, carry_len, carry_dist);
+  if (pb + 4 <= p1) {
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     u32x4 v = {out[0], out[1], out[2], out[3]};
-    *reinterpret_cast<u32x4 *>(res_out + (p - p0)) = v;
+    *reinterpret_cast<u32x4 *>(res_out + (pb - p0)) = v;
   } else {
-    for (uint32_t k = 0; k < 4 && p + k < p1; ++k) res_out[p - p0 + k] = out[k];
+    for (uint32_t k = 0; k < 4 && pb + k < p1; ++k) res_out[pb - p0 + k] = out[k];
   }
 }
 
@@ -302,7 +342,9 @@ __global__ __launch_bounds__(DF_THREADS) void match_kernel(DeflateParams P) {
   // a segment start (restart point) sees no history: its matches stay inside
   // the segment, so inflate can decode segments independently
   const bool restart = (b0 % P.restart) == 0 && (b0 > 0 || P.halo == 0);
-  const uint64_t h_lo = restart ? s_lo : (s_lo > DF_MAXDIST ? s_lo - DF_MAXDIST : 0);
+  // history: whole sub-chunks, so that the searched range starts on a sub-chunk
+  const uint64_t hist = restart ? 0 : (s_lo < (uint64_t)DF_HIST ? (s_lo & ~uint64_t(DF_SUB - 1)) : DF_HIST);
+  const uint64_t h_lo = s_lo - hist;
   const uint8_t *g = P.base + h_lo;  // rel 0
   const uint32_t rs = (uint32_t)(s_lo - h_lo), re = (uint32_t)(s_hi - h_lo);
   const uint32_t rend = (uint32_t)(P.end - h_lo);  // bytes available (for hashing)
@@ -1026,28 +1068,30 @@ __global__ __launch_bounds__(256) void stored_blocks(const uint8_t *__restrict__
 
 // ---- host launcher ---------------------------------------------------------------------------
 struct DeflateLevel {
-  int max_chain, nice, lazy, too_far, skip, klen, probe;
+  int max_chain, nice, lazy, too_far, skip, klen, probe, good;
 };
 
 static DeflateLevel level_params(int level) {
-  // tuning hook: ZT_DF_PARAMS="max_chain,nice,lazy,skip,klen,probe" overrides the level
+  // tuning hook: ZT_DF_PARAMS="max_chain,nice,lazy,skip,klen,probe[,good]" overrides the level
   if (const char *e = getenv("ZT_DF_PARAMS")) {
-    DeflateLevel L{64, 128, 1, 4096, 128, 3, 0};
-    if (sscanf(e, "%d,%d,%d,%d,%d,%d", &L.max_chain, &L.nice, &L.lazy, &L.skip, &L.klen, &L.probe) == 6) return L;
+    DeflateLevel L{64, 128, 1, 4096, 128, 8, 16, 8};
+    if (sscanf(e, "%d,%d,%d,%d,%d,%d,%d", &L.max_chain, &L.nice, &L.lazy, &L.skip, &L.klen, &L.probe, &L.good) >= 6)
+      return L;
   }
   switch (level) {
-    // {max_chain, nice, lazy, too_far, skip, klen, probe}: chains on 8-byte
-    // keys find the long matches (a 3-byte key chain of the same depth sees
-    // mostly candidates that cannot win); near probes find the short ones
-    case 1: return {4, 16, 0, 4096, 16, 8, 8};
-    case 2: return {8, 32, 0, 4096, 32, 8, 8};
-    case 3: return {16, 64, 0, 4096, 64, 8, 16};
-    case 4: return {16, 128, 1, 4096, 128, 8, 16};
-    case 5: return {24, 128, 1, 4096, 128, 8, 16};
-    case 7: return {64, 258, 1, 4096, 258, 8, 16};
-    case 8: return {128, 258, 1, 4096, 258, 8, 32};
-    case 9: return {512, 258, 1, 4096, 258, 8, 32};
-    default: return {32, 128, 1, 4096, 128, 8, 16};  // 6
+    // {max_chain, nice, lazy, too_far, skip, klen, probe, good}: chains on
+    // 8-byte keys find the long matches (a 3-byte key chain of the same depth
+    // sees mostly candidates that cannot win); near probes (registers) find
+    // the short ones; a carried match of `good` bytes cuts the chain to 1/4
+    case 1: return {4, 16, 0, 4096, 16, 8, 8, 4};
+    case 2: return {8, 32, 0, 4096, 32, 8, 8, 4};
+    case 3: return {16, 64, 0, 4096, 64, 8, 16, 4};
+    case 4: return {16, 128, 1, 4096, 128, 8, 16, 8};
+    case 5: return {24, 128, 1, 4096, 128, 8, 16, 8};
+    case 7: return {64, 258, 1, 4096, 258, 8, 16, 16};
+    case 8: return {128, 258, 1, 4096, 258, 8, 16, 32};
+    case 9: return {512, 258, 1, 4096, 258, 8, 16, 258};
+    default: return {32, 128, 1, 4096, 128, 8, 16, 8};  // 6
   }
 }
 
@@ -1121,6 +1165,7 @@ int deflate_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t halo, in
   P.skip_len = L.skip;
   P.klen = L.klen;
   P.probe = L.probe;
+  P.good = L.good;
   P.ctype = ctype;
   P.res = reinterpret_cast<uint32_t *>(sb);
   P.slots = sb + G.res_bytes;
