@@ -1087,11 +1087,11 @@ static DeflateLevel level_params(int level) {
     case 2: return {8, 32, 0, 4096, 32, 8, 8, 4};
     case 3: return {16, 64, 0, 4096, 64, 8, 16, 4};
     case 4: return {16, 128, 1, 4096, 128, 8, 16, 8};
-    case 5: return {24, 128, 1, 4096, 128, 8, 16, 8};
+    case 5: return {24, 128, 1, 4096, 128, 8, 16, 16};
     case 7: return {64, 258, 1, 4096, 258, 8, 16, 16};
     case 8: return {128, 258, 1, 4096, 258, 8, 16, 32};
     case 9: return {512, 258, 1, 4096, 258, 8, 16, 258};
-    default: return {32, 128, 1, 4096, 128, 8, 16, 8};  // 6
+    default: return {32, 128, 1, 4096, 128, 8, 16, 16};  // 6
   }
 }
 
