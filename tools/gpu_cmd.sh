@@ -1,3 +1,7 @@
-P="32,128,1,128,8,16,8 32,128,1,128,8,16,16 32,128,1,128,8,16,32 32,128,1,128,8,16,258 64,128,1,128,8,16,16 16,128,1,128,8,16,258 64,258,1,258,8,16,258 128,258,1,258,8,16,258 32,128,1,128,6,16,16 32,128,1,128,4,16,16 64,128,1,128,4,16,16"
+set -e
+timeout -k 10 600 python -m pytest tests -m gpu -x -q -k "deflate" > gpurun_out/t2.log 2>&1 || { tail -40 gpurun_out/t2.log; exit 1; }
+tail -2 gpurun_out/t2.log
+P="32,128,1,128,8,16,16 32,128,1,128,8,16,8 64,128,1,128,8,16,16"
 timeout -k 10 600 python tools/df_sweep.py wordsalad $P 2>&1 | grep -v amdgpu.ids
 timeout -k 10 600 python tools/df_sweep.py structured $P 2>&1 | grep -v amdgpu.ids
+timeout -k 10 600 python tools/df_sweep.py xorshift32 $P 2>&1 | grep -v amdgpu.ids

@@ -243,62 +243,85 @@ __device__ __forceinline__ void near_probe(const uint32_t (&w)[8], uint32_t cur0
   }
 }
 
-// longest match for position pb + K (carry: the previous position's match)
-template <int K>
-__device__ __forceinline__ uint32_t search_pos(const MatchShared *s, const DeflateParams &P, const uint32_t (&w)[8],
-                                               uint32_t pb, uint32_t p1, Key key, uint32_t &carry_len,
-                                               uint32_t &carry_dist) {
-  const uint32_t p = pb + K;
-  if (p >= p1) return 0;
-  const uint32_t klen = (uint32_t)P.klen;
-  const uint32_t max_len = (p1 - p) < 258 ? (p1 - p) : 258;
-  uint32_t best_len = 0, best_dist = 0;
-  if (max_len >= 3) {
-    if (carry_len > 3) {
-      best_len = carry_len - 1;
-      best_dist = carry_dist;
-    }
-    const uint32_t cur = win32<16 + K>(w);
-    const uint32_t cur2 = win32<20 + K>(w);
-    if ((int)best_len < P.skip_len && max_len >= klen) {
-      // a good carried match needs only a short look for a better one
-      const int max_hops = (int)best_len >= P.good ? (P.max_chain >> 2) : P.max_chain;
-      // the word ending at best_len: a candidate can only win if it matches there
-      uint32_t o = best_len >= 4 ? best_len - 3 : 0;
-      uint32_t pw = best_len >= 4 ? ld32(s, p + o) : 0u;
-      uint32_t link = s->prev[ridx(p)];
-      uint32_t q = p;
-      int hops = 0;
-#pragma unroll 1
-      while (link && hops < max_hops) {
-        q -= link;
-        if (p - q > DF_MAXDIST) break;
-        ++hops;
-        link = s->prev[ridx(q)];
-        if (best_len >= 4 && ld32(s, q + o) != pw) continue;
-        if (((ld32(s, q) ^ cur) & key.kmask) != 0) continue;
-        if (key.kmask2 && ((ld32(s, q + 4) ^ cur2) & key.kmask2) != 0) continue;
-        uint32_t len = klen;
-        while (len < max_len) {
-          uint32_t x = ld32(s, q + len) ^ ld32(s, p + len);
-          if (x) {
-            len += (uint32_t)(__ffs(x) - 1) >> 3;
-            break;
-          }
-          len += 4;
-        }
-        if (len > max_len) len = max_len;
-        if (len > best_len) {
-          best_len = len;
-          best_dist = p - q;
-          if ((int)len >= P.nice_len || len >= max_len) break;
-          o = len - 3;
-          pw = ld32(s, p + o);
-        }
-      }
-    }
-    if (best_len < klen) near_probe<K, 1>(w, cur, cur2, p, max_len, P.probe, best_len, best_dist);
+// One position's hash-chain walk (newest candidate first).  Two walks are
+// interleaved per thread so that their dependent LDS loads overlap.
+struct Walk {
+  uint32_t p, q, link, max_len, best_len, best_dist, o, pw, cur, cur2;
+  int hops, max_hops;
+  bool active;
+};
+
+// start the walk of position p (carry: the previous position's match)
+__device__ __forceinline__ void walk_init(Walk &w, const MatchShared *s, const DeflateParams &P, uint32_t p, uint32_t p1,
+                                          uint32_t cur, uint32_t cur2, uint32_t carry_len, uint32_t carry_dist) {
+  w.p = p;
+  w.q = p;
+  w.cur = cur;
+  w.cur2 = cur2;
+  w.max_len = p < p1 ? ((p1 - p) < 258 ? (p1 - p) : 258) : 0;
+  w.best_len = 0;
+  w.best_dist = 0;
+  if (carry_len > 3 && w.max_len >= 3) {
+    w.best_len = carry_len - 1 < w.max_len ? carry_len - 1 : w.max_len;
+    w.best_dist = carry_dist;
   }
+  w.hops = 0;
+  w.max_hops = (int)w.best_len >= P.good ? (P.max_chain >> 2) : P.max_chain;
+  w.active = w.max_len >= (uint32_t)P.klen && (int)w.best_len < P.skip_len;
+  w.o = w.best_len >= 4 ? w.best_len - 3 : 0;
+  w.pw = 0;
+  w.link = 0;
+  if (w.active) {
+    // the word ending at best_len: a candidate can only win if it matches there
+    w.pw = w.best_len >= 4 ? ld32(s, p + w.o) : 0u;
+    w.link = s->prev[ridx(p)];
+    w.active = w.link != 0;
+  }
+}
+
+__device__ __forceinline__ void walk_step(Walk &w, const MatchShared *s, const DeflateParams &P, Key key) {
+  if (!w.active) return;
+  w.q -= w.link;
+  if (w.p - w.q > DF_MAXDIST) {
+    w.active = false;
+    return;
+  }
+  ++w.hops;
+  const uint32_t q = w.q;
+  w.link = s->prev[ridx(q)];
+  w.active = w.link != 0 && w.hops < w.max_hops;
+  if (w.best_len >= 4 && ld32(s, q + w.o) != w.pw) return;
+  if (((ld32(s, q) ^ w.cur) & key.kmask) != 0) return;
+  if (key.kmask2 && ((ld32(s, q + 4) ^ w.cur2) & key.kmask2) != 0) return;
+  uint32_t len = (uint32_t)P.klen;
+  while (len < w.max_len) {
+    const uint32_t x = ld32(s, q + len) ^ ld32(s, w.p + len);
+    if (x) {
+      len += (uint32_t)(__ffs(x) - 1) >> 3;
+      break;
+    }
+    len += 4;
+  }
+  if (len > w.max_len) len = w.max_len;
+  if (len > w.best_len) {
+    w.best_len = len;
+    w.best_dist = w.p - q;
+    if ((int)len >= P.nice_len || len >= w.max_len) {
+      w.active = false;
+      return;
+    }
+    w.o = len - 3;
+    w.pw = ld32(s, w.p + w.o);
+  }
+}
+
+// finish position pb + K: near probes when the chain found nothing long
+template <int K>
+__device__ __forceinline__ uint32_t walk_finish(const Walk &w, const DeflateParams &P, const uint32_t (&win)[8],
+                                                uint32_t &carry_len, uint32_t &carry_dist) {
+  uint32_t best_len = w.best_len, best_dist = w.best_dist;
+  if (w.max_len >= 3 && best_len < (uint32_t)P.klen)
+    near_probe<K, 1>(win, w.cur, w.cur2, w.p, w.max_len, P.probe, best_len, best_dist);
   carry_len = best_len;
   carry_dist = best_dist;
   if (best_len == 3 && best_dist > (uint32_t)P.too_far) best_len = 0;
@@ -316,12 +339,26 @@ __device__ void search_sub(const MatchShared *s, const DeflateParams &P, uint32_
   uint32_t w[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) w[i] = s->ring[ridx(pb - 16 + 4 * i) >> 2];
-  uint32_t carry_len = 0, carry_dist = 0;
+  // positions 0 and 2 walk together, then 1 and 3 with the carry of 0 and 2
   uint32_t out[4];
-  out[0] = search_pos<0>(s, P, w, pb, p1, key, carry_len, carry_dist);
-  out[1] = search_pos<1>(s, P, w, pb, p1, key, carry_len, carry_dist);
-  out[2] = search_pos<2>(s, P, w, pb, p1, key, carry_len, carry_dist);
-  out[3] = search_pos<3>(s, P, w, pb, p1, key, carry_len, carry_dist);
+  uint32_t c0l, c0d, c2l, c2d, cl, cd;
+  Walk wa, wb;
+  walk_init(wa, s, P, pb, p1, win32<16>(w), win32<20>(w), 0, 0);
+  walk_init(wb, s, P, pb + 2, p1, win32<18>(w), win32<22>(w), 0, 0);
+  while (wa.active || wb.active) {
+    walk_step(wa, s, P, key);
+    walk_step(wb, s, P, key);
+  }
+  out[0] = walk_finish<0>(wa, P, w, c0l, c0d);
+  out[2] = walk_finish<2>(wb, P, w, c2l, c2d);
+  walk_init(wa, s, P, pb + 1, p1, win32<17>(w), win32<21>(w), c0l, c0d);
+  walk_init(wb, s, P, pb + 3, p1, win32<19>(w), win32<23>(w), c2l, c2d);
+  while (wa.active || wb.active) {
+    walk_step(wa, s, P, key);
+    walk_step(wb, s, P, key);
+  }
+  out[1] = walk_finish<1>(wa, P, w, cl, cd);
+  out[3] = walk_finish<3>(wb, P, w, cl, cd);
   if (pb + 4 <= p1) {
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     u32x4 v = {out[0], out[1], out[2], out[3]};
