@@ -1132,8 +1132,9 @@ static DeflateLevel level_params(int level) {
   }
 }
 
-// Work split: enough workgroups to cover every CU twice, at most 32 blocks
-// (1 MiB) per workgroup, a power of two so segments (32 blocks) align.
+// Work split: enough workgroups to cover every CU twice, at most 8 blocks
+// (256 KiB) per workgroup (small super-chunks balance uneven data across
+// CUs; each loads 28 KiB of history), a power of two so segments (32 blocks) align.
 struct DeflateGeom {
   uint32_t nblocks, k, nwg;
   size_t res_bytes, slot_bytes, len_bytes, off_bytes, plan_bytes;
@@ -1143,8 +1144,11 @@ static size_t deflate_geometry(const DeviceCtx *c, size_t n, DeflateGeom *g) {
   g->nblocks = (uint32_t)((n + DF_BLOCK - 1) / DF_BLOCK);
   if (g->nblocks == 0) g->nblocks = 1;
   uint32_t kk = (g->nblocks + 2 * c->num_cu - 1) / (2 * c->num_cu);
+  // tuning hook: ZT_DF_SUPER caps the blocks per workgroup (power of two <= 32)
+  static const int cap_env = getenv("ZT_DF_SUPER") ? atoi(getenv("ZT_DF_SUPER")) : 0;
+  const uint32_t cap = cap_env > 0 && cap_env <= 32 ? (uint32_t)cap_env : 8u;
   uint32_t k2 = 1;
-  while (k2 < kk && k2 < 32) k2 <<= 1;
+  while (k2 < kk && k2 < cap) k2 <<= 1;
   g->k = k2;
   g->nwg = (g->nblocks + k2 - 1) / k2;
   g->res_bytes = ((size_t)g->nblocks * DF_BLOCK * 4 + 255) & ~size_t(255);
