@@ -188,7 +188,7 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   // 3. the chain from the stream start, cut into segments at restart markers
   std::vector<ChainUnit> chain;
   std::vector<SegJob> segs;
-  uint64_t total = 0;
+  uint64_t total = 0, seg_start = 0, desc_total = 0, desc_seg = 0;
   size_t u = 0;
   for (;;) {
     const TokResult &r = res[u];
@@ -196,11 +196,18 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
       FALLBACK("unit %zu (start %llu, chain %zu): status %d detail %d ntok %u out %llu\n", u,
                (unsigned long long)jobs[u].start, chain.size(), r.status, r.detail, r.ntok,
                (unsigned long long)r.out_len);
-    const bool seg_start = u == 0 || restart[u - 1];
-    if (seg_start || segs.empty()) segs.push_back(SegJob{(uint32_t)chain.size(), 0});
-    chain.push_back(ChainUnit{jobs[u].tok_off, total, r.ntok, (uint32_t)r.out_len});
+    const bool seg_start_here = u == 0 || restart[u - 1];
+    if (seg_start_here || segs.empty()) {
+      desc_total = (desc_total + 127) & ~uint64_t(127);
+      desc_seg = desc_total;
+      seg_start = total;
+      segs.push_back(SegJob{(uint32_t)chain.size(), 0});
+    }
+    chain.push_back(ChainUnit{jobs[u].tok_off, total, seg_start, desc_seg + (total - seg_start), r.ntok,
+                              (uint32_t)r.out_len});
     segs.back().count++;
     total += r.out_len;
+    desc_total = desc_seg + (total - seg_start);
     if (r.stop_idx < 0) break;
     const size_t nx = (size_t)r.stop_idx + 1;
     if (nx <= u || nx >= units) FALLBACK("unit %zu: bad stop %d\n", u, r.stop_idx);
@@ -217,14 +224,17 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   } else if (total > out_cap) {
     return set_error(ZT_E_ARG, "output capacity too small");
   }
-  // 4. resolve, one wave per segment
-  void *d_chain;
+  // 4. expand (one wave per unit) and copy (one wave per segment)
+  void *d_chain, *d_desc;
   const size_t chain_bytes = align256(chain.size() * sizeof(ChainUnit));
   const size_t seg_bytes = align256(segs.size() * sizeof(SegJob));
-  ZT_TRY(scratch(c, 7, chain_bytes + seg_bytes + align256(segs.size() * 4), &d_chain));
+  const size_t ust_bytes = align256(chain.size() * 4);
+  ZT_TRY(scratch(c, 7, chain_bytes + seg_bytes + ust_bytes + align256(segs.size() * 4), &d_chain));
+  ZT_TRY(scratch(c, 3, (desc_total + 256) * 2, &d_desc));  // + slack: chunked descriptor reads
   ChainUnit *d_cu = static_cast<ChainUnit *>(d_chain);
   SegJob *d_sj = reinterpret_cast<SegJob *>(static_cast<uint8_t *>(d_chain) + chain_bytes);
-  int32_t *d_st = reinterpret_cast<int32_t *>(static_cast<uint8_t *>(d_chain) + chain_bytes + seg_bytes);
+  int32_t *d_ust = reinterpret_cast<int32_t *>(static_cast<uint8_t *>(d_chain) + chain_bytes + seg_bytes);
+  int32_t *d_st = reinterpret_cast<int32_t *>(static_cast<uint8_t *>(d_chain) + chain_bytes + seg_bytes + ust_bytes);
   ZT_HIP(hipMemcpyAsync(d_cu, chain.data(), chain.size() * sizeof(ChainUnit), hipMemcpyHostToDevice, s));
   ZT_HIP(hipMemcpyAsync(d_sj, segs.data(), segs.size() * sizeof(SegJob), hipMemcpyHostToDevice, s));
   ResolveParams rp;
@@ -232,15 +242,22 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   rp.units = d_cu;
   rp.segs = d_sj;
   rp.out = d_out;
+  rp.desc = static_cast<uint16_t *>(d_desc);
+  rp.unit_status = d_ust;
   rp.seg_status = d_st;
+  rp.nunits = (uint32_t)chain.size();
   rp.nseg = (uint32_t)segs.size();
   ZT_TRY(resolve_segments_dev(rp, s));
   ZT_TRY(timing_end(c, s, 2));
+  std::vector<int32_t> ust(chain.size());
+  ZT_HIP(hipMemcpyAsync(ust.data(), d_ust, chain.size() * 4, hipMemcpyDeviceToHost, s));
   std::vector<int32_t> st(segs.size());
   ZT_HIP(hipMemcpyAsync(st.data(), d_st, segs.size() * 4, hipMemcpyDeviceToHost, s));
   ZT_HIP(hipStreamSynchronize(s));
   ZT_TRY(timing_collect(c, &c->times.inflate_ms, &c->times.inflate_launches, 2));
   ZT_TRY(timing_collect(c, &c->times.inflate_tok_ms, &c->times.inflate_toks, 3));
+  for (size_t i = 0; i < ust.size(); ++i)
+    if (ust[i] != ZT_OK) FALLBACK("unit %zu of %zu (chain): status %d\n", i, ust.size(), ust[i]);
   for (size_t i = 0; i < st.size(); ++i)
     if (st[i] != ZT_OK) FALLBACK("segment %zu of %zu: status %d\n", i, st.size(), st[i]);
   return ZT_OK;

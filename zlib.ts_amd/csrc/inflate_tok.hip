@@ -628,16 +628,105 @@ constexpr uint32_t RS_TOK_RING = 1024;        // tokens staged in LDS (16 chunks
 constexpr uint32_t RS_AHEAD = 12;             // chunks in flight ahead of the cursor
 constexpr uint32_t RS_FLUSH = 8192;           // output flush granule
 
-struct ResolveShared {
-  uint8_t ring[RING];          // 32 KiB history, also the output staging
+// Phase B runs in two kernels.
+//
+// B0 expand_kernel -- one wavefront per unit (many per CU: no history
+//   needed): tokens -> one u16 *descriptor* per output byte, written at the
+//   byte's final position: 0x8000 | byte for a literal, else D - 1 where the
+//   byte equals the output byte D positions back.  For byte k of a match
+//   (length L, distance d) the source is taken before the match start,
+//   start - d + (k mod d), so D = d * (1 + k / d) <= 32768, and a match never
+//   depends on itself.  64 bytes per step: each lane finds its token with a
+//   start-mark ballot over the scanned token lengths.
+// B1 copy_kernel -- one wavefront per segment, sequential over its bytes,
+//   64 per step: a literal, or a read of the 32 KiB LDS history ring; bytes
+//   whose source lies inside the step are resolved by pointer jumping.  The
+//   output goes through the ring to HBM in 8 KiB granules.
+struct ExpandShared {
   uint32_t tok[RS_TOK_RING];   // token chunks, filled by LDS-DMA
   uint32_t mark[64];
 };
 
+__global__ __launch_bounds__(64) void expand_kernel(ResolveParams P) {
+  __shared__ ExpandShared sh;
+  const uint32_t u = blockIdx.x;
+  const int lane = threadIdx.x & 63;
+  const ChainUnit cu = P.units[u];
+  const uint32_t *tk = P.tokens + cu.tok_off;
+  const uint32_t ntok = cu.ntok;
+  const uint32_t nchunks = (ntok + 63) / 64;
+  uint16_t *desc = P.desc + cu.desc_off;
+  const uint64_t back = cu.out_off - cu.seg_off;  // bytes of the segment before this unit
+  sh.mark[lane] = 0;
+  uint32_t seq = 0;
+  uint32_t issued = 0;
+  uint32_t cur = 0, rem = 0;
+  uint32_t op = 0;  // unit-relative output position
+  bool bad = false;
+  while (cur < ntok) {
+    const uint32_t need = (cur >> 6) + 2 < nchunks ? (cur >> 6) + 2 : nchunks;
+    const uint32_t want = need + RS_AHEAD < nchunks ? need + RS_AHEAD : nchunks;
+    while (issued < want) {
+      __builtin_amdgcn_global_load_lds(tk + (uint64_t)issued * 64 + lane,
+                                       &sh.tok[(issued * 64) & (RS_TOK_RING - 1)], 4, 0, 0);
+      ++issued;
+    }
+    if (issued - need >= RS_AHEAD)
+      __builtin_amdgcn_s_waitcnt(0x0F70 | RS_AHEAD);  // vmcnt(RS_AHEAD)
+    else
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    const uint32_t ti = cur + (uint32_t)lane;
+    const bool valid = ti < ntok;
+    const uint32_t t = sh.tok[ti & (RS_TOK_RING - 1)];
+    const uint32_t len = valid ? tok_len(t) : 0u;
+    const uint32_t S = wave_incl_scan(len);
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)S, 63) - rem;
+    const uint32_t W = total < 64 ? total : 64;
+    ++seq;
+    const int32_t p = (int32_t)S - (int32_t)rem;
+    if (valid && p > 0 && p < 64) sh.mark[p] = seq;
+    wave_sync();
+    const uint64_t starts = __ballot(sh.mark[lane] == seq);
+    const uint32_t owner = __popcll(starts & (~0ull >> (63 - lane)));  // token of byte `lane`
+    const uint32_t tj = bperm(t, owner);
+    const uint32_t ej = bperm(S - len, owner);  // the token's start, relative to the cursor token
+    if ((uint32_t)lane < W) {
+      uint32_t dsc;
+      if ((tj >> 16) == 0) {
+        dsc = 0x8000u | (tj & 0xFF);
+      } else {
+        const uint32_t dist = tj & 0xFFFF;
+        const uint32_t k = rem + (uint32_t)lane - ej;  // byte index inside the match
+        const uint32_t D = k < dist ? dist : dist * (1 + k / dist);
+        // the source must lie inside the segment
+        if ((uint64_t)D > back + op + lane) bad = true;
+        dsc = D - 1;
+      }
+      desc[op + lane] = (uint16_t)dsc;
+    }
+    op += W;
+    const uint64_t done = __ballot(valid && S <= rem + W);
+    const uint32_t kdone = (uint32_t)__popcll(done);
+    const uint32_t s_last = kdone ? (uint32_t)__builtin_amdgcn_readlane((int)S, kdone - 1) : 0u;
+    rem = rem + W - s_last;
+    cur += kdone;
+  }
+  const bool any_bad = __ballot(bad) != 0;
+  if (lane == 0) P.unit_status[u] = any_bad ? ZT_E_INVALID_DISTANCE : (op != cu.out_len ? ZT_E_INPUT_BROKEN : ZT_OK);
+}
+
 typedef unsigned int u32x4r __attribute__((ext_vector_type(4)));
 
-// ring bytes [lo, hi) (segment positions) to out + lo (out 16-aligned when possible)
-__device__ __forceinline__ void rs_flush(const ResolveShared *sh, uint8_t *out, uint64_t lo, uint64_t hi, int lane) {
+constexpr uint32_t CP_DESC_RING = 2048;  // descriptors staged in LDS (16 chunks of 128)
+constexpr uint32_t CP_AHEAD = 12;
+
+struct CopyShared {
+  uint8_t ring[RING];                        // 32 KiB history, also the output staging
+  uint16_t desc[CP_DESC_RING];               // descriptor chunks, filled by LDS-DMA
+};
+
+// ring bytes [lo, hi) (segment positions) to out + lo
+__device__ __forceinline__ void cp_flush(const CopyShared *sh, uint8_t *out, uint64_t lo, uint64_t hi, int lane) {
   if (lo >= hi) return;
   if ((((uintptr_t)out + lo) & 15) == 0 && ((hi - lo) & 15) == 0) {
     for (uint64_t p = lo + (uint64_t)lane * 16; p < hi; p += 1024)
@@ -647,117 +736,71 @@ __device__ __forceinline__ void rs_flush(const ResolveShared *sh, uint8_t *out, 
   }
 }
 
-__global__ __launch_bounds__(64) void resolve_kernel(ResolveParams P) {
-  __shared__ ResolveShared sh;
+__global__ __launch_bounds__(64) void copy_kernel(ResolveParams P) {
+  __shared__ CopyShared sh;
   const uint32_t sg = blockIdx.x;
   const int lane = threadIdx.x & 63;
   const SegJob sj = P.segs[sg];
   const uint64_t seg_out = P.units[sj.first].out_off;
+  const ChainUnit lastu = P.units[sj.first + sj.count - 1];
+  const uint64_t n = lastu.out_off + lastu.out_len - seg_out;  // segment bytes
   uint8_t *out = P.out + seg_out;
-  sh.mark[lane] = 0;
-  uint32_t seq = 0;
-  uint64_t op = 0;       // segment-relative output position
-  uint64_t flushed = 0;  // bytes [0, flushed) are in HBM
-  int status = ZT_OK;
-  for (uint32_t k = 0; k < sj.count && status == ZT_OK; ++k) {
-    const ChainUnit cu = P.units[sj.first + k];
-    const uint32_t *tk = P.tokens + cu.tok_off;
-    const uint32_t ntok = cu.ntok;
-    const uint32_t nchunks = (ntok + 63) / 64;
-    uint32_t issued = 0;  // token chunks requested for this unit
-    uint32_t cur = 0, rem = 0;
-    const uint64_t op_unit = op;
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // nothing of the previous unit in flight
-    while (cur < ntok) {
-      // ---- tokens [cur, cur + 64) must be in LDS: chunks < need landed
-      const uint32_t need = (cur >> 6) + 2 < nchunks ? (cur >> 6) + 2 : nchunks;
-      const uint32_t want = need + RS_AHEAD < nchunks ? need + RS_AHEAD : nchunks;
-      while (issued < want) {
-        __builtin_amdgcn_global_load_lds(tk + (uint64_t)issued * 64 + lane,
-                                         &sh.tok[(issued * 64) & (RS_TOK_RING - 1)], 4, 0, 0);
-        ++issued;
-      }
-      if (issued - need >= RS_AHEAD)
-        __builtin_amdgcn_s_waitcnt(0x0F70 | RS_AHEAD);  // vmcnt(RS_AHEAD)
-      else
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-      const uint32_t ti = cur + (uint32_t)lane;
-      const bool valid = ti < ntok;
-      const uint32_t t = sh.tok[ti & (RS_TOK_RING - 1)];
-      const uint32_t len = valid ? tok_len(t) : 0u;
-      const uint32_t S = wave_incl_scan(len);
-      const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)S, 63) - rem;
-      const uint32_t W = total < 64 ? total : 64;
-      // token i + 1 starts at S_i - rem inside the window
-      ++seq;
-      const int32_t p = (int32_t)S - (int32_t)rem;
-      if (valid && p > 0 && p < 64) sh.mark[p] = seq;
-      wave_sync();
-      const uint64_t starts = __ballot(sh.mark[lane] == seq);
-      const uint32_t owner = __popcll(starts & (~0ull >> (63 - lane)));  // token of byte `lane`
-      const uint32_t tj = bperm(t, owner);
-      const uint32_t sj_ = bperm(S - len, owner);  // its start (before rem)
-      uint32_t val = 0;
-      int32_t ptr = -1;
-      bool bad = false;
-      if ((uint32_t)lane < W) {
-        if ((tj >> 16) == 0) {
-          val = tj & 0xFF;
-        } else {
-          const uint32_t dist = tj & 0xFFFF;
-          // byte k of a match is history[start - dist + k mod dist]: it depends
-          // only on bytes before the match
-          const uint64_t tstart = op + (uint64_t)lane - ((uint64_t)rem + lane - sj_);
-          const uint32_t kk = rem + (uint32_t)lane - sj_;
-          const uint64_t src = tstart - dist + (kk < dist ? kk : kk % dist);
-          if (dist > tstart) {
-            bad = true;  // reaches behind the segment start
-          } else if (src >= op) {
-            ptr = (int32_t)(src - op);
-          } else {
-            val = sh.ring[src & RING_MASK];
-          }
-        }
-      }
-      if (__ballot(bad)) {
-        status = ZT_E_INVALID_DISTANCE;
-        break;
-      }
-      // in-window references: pointer jumping (a source lane precedes its reader)
-      while (__ballot(ptr >= 0)) {
-        const uint32_t q = ptr >= 0 ? (uint32_t)ptr : (uint32_t)lane;
-        const uint32_t v2 = bperm(val, q);
-        const int32_t p2 = (int32_t)bperm((uint32_t)ptr, q);
-        if (ptr >= 0) {
-          if (p2 < 0) {
-            val = v2;
-            ptr = -1;
-          } else {
-            ptr = p2;
-          }
-        }
-      }
-      if ((uint32_t)lane < W) sh.ring[(op + lane) & RING_MASK] = (uint8_t)val;
-      wave_sync();
-      op += W;
-      if (op - flushed >= RS_FLUSH) {
-        const uint64_t upto = flushed + RS_FLUSH;
-        rs_flush(&sh, out, flushed, upto, lane);
-        flushed = upto;
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // keep vmcnt counting token chunks only
-      }
-      // advance past the tokens that end inside this window
-      const uint64_t done = __ballot(valid && S <= rem + W);
-      const uint32_t kdone = (uint32_t)__popcll(done);
-      const uint32_t s_last = kdone ? (uint32_t)__builtin_amdgcn_readlane((int)S, kdone - 1) : 0u;
-      rem = rem + W - s_last;
-      cur += kdone;
+  const uint16_t *dsrc = P.desc + P.units[sj.first].desc_off;  // 128-aligned
+  // descriptor chunk c = bytes [128 c, 128 c + 128): two per lane, one DMA of 4 bytes per lane
+  const uint64_t nchunks = (n + 127) / 128;
+  uint64_t issued = 0;
+  uint64_t flushed = 0;
+  for (uint64_t op = 0; op < n; op += 64) {
+    const uint64_t need = (op >> 7) + 1 < nchunks ? (op >> 7) + 1 : nchunks;
+    const uint64_t want = need + CP_AHEAD < nchunks ? need + CP_AHEAD : nchunks;
+    while (issued < want) {
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint32_t *>(dsrc + issued * 128) + lane,
+                                       &sh.desc[(issued * 128) & (CP_DESC_RING - 1)], 4, 0, 0);
+      ++issued;
     }
-    if (op - op_unit != cu.out_len) status = ZT_E_INPUT_BROKEN;
+    if (issued - need >= CP_AHEAD)
+      __builtin_amdgcn_s_waitcnt(0x0F70 | CP_AHEAD);
+    else
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+    const uint64_t x = op + (uint64_t)lane;
+    const bool in = x < n;
+    const uint32_t d = in ? sh.desc[x & (CP_DESC_RING - 1)] : 0x8000u;
+    uint32_t val = d & 0xFF;
+    int32_t ptr = -1;
+    if (!(d & 0x8000u)) {
+      const uint64_t src = x - (d + 1);
+      if (src < op)
+        val = sh.ring[src & RING_MASK];
+      else
+        ptr = (int32_t)(src - op);
+    }
+    // in-step references: pointer jumping (a source lane precedes its reader)
+    while (__ballot(ptr >= 0)) {
+      const uint32_t q = ptr >= 0 ? (uint32_t)ptr : (uint32_t)lane;
+      const uint32_t v2 = bperm(val, q);
+      const int32_t p2 = (int32_t)bperm((uint32_t)ptr, q);
+      if (ptr >= 0) {
+        if (p2 < 0) {
+          val = v2;
+          ptr = -1;
+        } else {
+          ptr = p2;
+        }
+      }
+    }
+    if (in) sh.ring[x & RING_MASK] = (uint8_t)val;
+    wave_sync();
+    const uint64_t end = op + 64 < n ? op + 64 : n;
+    if (end - flushed >= RS_FLUSH) {
+      const uint64_t upto = flushed + RS_FLUSH;
+      cp_flush(&sh, out, flushed, upto, lane);
+      flushed = upto;
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // keep vmcnt counting descriptor chunks only
+    }
   }
   wave_sync();
-  if (status == ZT_OK) rs_flush(&sh, out, flushed, op, lane);
-  if (lane == 0) P.seg_status[sg] = status;
+  cp_flush(&sh, out, flushed, n, lane);
+  if (lane == 0) P.seg_status[sg] = ZT_OK;
 }
 
 }  // namespace
@@ -771,7 +814,9 @@ int tokenize_units_dev(const TokParams &p, hipStream_t s) {
 
 int resolve_segments_dev(const ResolveParams &p, hipStream_t s) {
   if (p.nseg == 0) return ZT_OK;
-  resolve_kernel<<<p.nseg, 64, 0, s>>>(p);
+  expand_kernel<<<p.nunits, 64, 0, s>>>(p);
+  ZT_HIP(hipGetLastError());
+  copy_kernel<<<p.nseg, 64, 0, s>>>(p);
   ZT_HIP(hipGetLastError());
   return ZT_OK;
 }

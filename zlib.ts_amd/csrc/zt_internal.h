@@ -177,6 +177,8 @@ struct TokParams {
 struct ChainUnit {
   uint64_t tok_off;
   uint64_t out_off;  // absolute output offset
+  uint64_t seg_off;  // output offset of the unit's segment
+  uint64_t desc_off; // its descriptors (segments start 128-aligned)
   uint32_t ntok;
   uint32_t out_len;
 };
@@ -188,7 +190,10 @@ struct ResolveParams {
   const ChainUnit *units;
   const SegJob *segs;
   uint8_t *out;
-  int32_t *seg_status;
+  uint16_t *desc;        // one descriptor per output byte (expand -> copy)
+  int32_t *unit_status;  // expand
+  int32_t *seg_status;   // copy
+  uint32_t nunits;
   uint32_t nseg;
 };
 int tokenize_units_dev(const TokParams &p, hipStream_t s);
