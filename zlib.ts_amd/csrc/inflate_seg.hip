@@ -198,7 +198,7 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
                (unsigned long long)r.out_len);
     const bool seg_start_here = u == 0 || restart[u - 1];
     if (seg_start_here || segs.empty()) {
-      desc_total = (desc_total + 127) & ~uint64_t(127);
+      desc_total = (desc_total + 511) & ~uint64_t(511);
       desc_seg = desc_total;
       seg_start = total;
       segs.push_back(SegJob{(uint32_t)chain.size(), 0});
@@ -230,7 +230,7 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   const size_t seg_bytes = align256(segs.size() * sizeof(SegJob));
   const size_t ust_bytes = align256(chain.size() * 4);
   ZT_TRY(scratch(c, 7, chain_bytes + seg_bytes + ust_bytes + align256(segs.size() * 4), &d_chain));
-  ZT_TRY(scratch(c, 3, (desc_total + 256) * 2, &d_desc));  // + slack: chunked descriptor reads
+  ZT_TRY(scratch(c, 3, (desc_total + 1024) * 2, &d_desc));  // + slack: chunked descriptor reads
   ChainUnit *d_cu = static_cast<ChainUnit *>(d_chain);
   SegJob *d_sj = reinterpret_cast<SegJob *>(static_cast<uint8_t *>(d_chain) + chain_bytes);
   int32_t *d_ust = reinterpret_cast<int32_t *>(static_cast<uint8_t *>(d_chain) + chain_bytes + seg_bytes);

@@ -642,9 +642,12 @@ constexpr uint32_t RS_FLUSH = 8192;           // output flush granule
 //   64 per step: a literal, or a read of the 32 KiB LDS history ring; bytes
 //   whose source lies inside the step are resolved by pointer jumping.  The
 //   output goes through the ring to HBM in 8 KiB granules.
+constexpr uint32_t CP_STEP = 256;  // copy_kernel bytes per step
+
 struct ExpandShared {
   uint32_t tok[RS_TOK_RING];   // token chunks, filled by LDS-DMA
   uint32_t mark[64];
+  uint16_t cw[CP_STEP];        // descriptors of the current copy step
 };
 
 __global__ __launch_bounds__(64) void expand_kernel(ResolveParams P) {
@@ -681,7 +684,11 @@ __global__ __launch_bounds__(64) void expand_kernel(ResolveParams P) {
     const uint32_t len = valid ? tok_len(t) : 0u;
     const uint32_t S = wave_incl_scan(len);
     const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)S, 63) - rem;
-    const uint32_t W = total < 64 ? total : 64;
+    // windows coincide with copy_kernel's 64-byte steps of the segment
+    const uint64_t pos = back + op;  // segment position of this window's first byte
+    const uint32_t room = 64 - (uint32_t)(pos & 63);
+    const uint32_t W = total < room ? total : room;
+    const uint64_t ws = pos & ~uint64_t(CP_STEP - 1);
     ++seq;
     const int32_t p = (int32_t)S - (int32_t)rem;
     if (valid && p > 0 && p < 64) sh.mark[p] = seq;
@@ -690,20 +697,53 @@ __global__ __launch_bounds__(64) void expand_kernel(ResolveParams P) {
     const uint32_t owner = __popcll(starts & (~0ull >> (63 - lane)));  // token of byte `lane`
     const uint32_t tj = bperm(t, owner);
     const uint32_t ej = bperm(S - len, owner);  // the token's start, relative to the cursor token
+    // descriptor: 0x8000 | byte (literal), 0x8100 | o (= byte ws + o, before
+    // this unit), or ws - src - 1 (a byte before the copy step); references
+    // into the step are followed here (earlier windows from LDS, this window
+    // by pointer jumping over the lanes)
+    uint32_t dsc = 0x8000u;
+    int32_t ptr = -1;
     if ((uint32_t)lane < W) {
-      uint32_t dsc;
       if ((tj >> 16) == 0) {
         dsc = 0x8000u | (tj & 0xFF);
       } else {
         const uint32_t dist = tj & 0xFFFF;
         const uint32_t k = rem + (uint32_t)lane - ej;  // byte index inside the match
         const uint32_t D = k < dist ? dist : dist * (1 + k / dist);
-        // the source must lie inside the segment
-        if ((uint64_t)D > back + op + lane) bad = true;
-        dsc = D - 1;
+        const uint64_t x = pos + lane;
+        if ((uint64_t)D > x) {
+          bad = true;  // reaches behind the segment start
+        } else {
+          const uint64_t src = x - D;
+          if (src < ws)
+            dsc = (uint32_t)(ws - src - 1);
+          else if (src < back)
+            dsc = 0x8100u | (uint32_t)(src - ws);  // before this unit: copy_kernel resolves it
+          else if (src < pos)
+            dsc = sh.cw[src - ws];  // an earlier window of this step, already resolved
+          else
+            ptr = (int32_t)(src - pos);
+        }
       }
-      desc[op + lane] = (uint16_t)dsc;
     }
+    while (__ballot(ptr >= 0)) {
+      const uint32_t q = ptr >= 0 ? (uint32_t)ptr : (uint32_t)lane;
+      const uint32_t d2 = bperm(dsc, q);
+      const int32_t p2 = (int32_t)bperm((uint32_t)ptr, q);
+      if (ptr >= 0) {
+        if (p2 < 0) {
+          dsc = d2;
+          ptr = -1;
+        } else {
+          ptr = p2;
+        }
+      }
+    }
+    if ((uint32_t)lane < W) {
+      desc[op + lane] = (uint16_t)dsc;
+      sh.cw[pos - ws + lane] = (uint16_t)dsc;
+    }
+    wave_sync();
     op += W;
     const uint64_t done = __ballot(valid && S <= rem + W);
     const uint32_t kdone = (uint32_t)__popcll(done);
@@ -736,6 +776,14 @@ __device__ __forceinline__ void cp_flush(const CopyShared *sh, uint8_t *out, uin
   }
 }
 
+// one descriptor -> byte, or -1 for "the byte op + off of this step"
+__device__ __forceinline__ uint32_t cp_byte(const CopyShared *sh, uint64_t op, uint32_t d, int32_t &off) {
+  off = -1;
+  if (!(d & 0x8000u)) return sh->ring[(op - d - 1) & RING_MASK];
+  if (d & 0x100u) off = (int32_t)(d & 0xFF);
+  return d & 0xFF;
+}
+
 __global__ __launch_bounds__(64) void copy_kernel(ResolveParams P) {
   __shared__ CopyShared sh;
   const uint32_t sg = blockIdx.x;
@@ -745,13 +793,13 @@ __global__ __launch_bounds__(64) void copy_kernel(ResolveParams P) {
   const ChainUnit lastu = P.units[sj.first + sj.count - 1];
   const uint64_t n = lastu.out_off + lastu.out_len - seg_out;  // segment bytes
   uint8_t *out = P.out + seg_out;
-  const uint16_t *dsrc = P.desc + P.units[sj.first].desc_off;  // 128-aligned
-  // descriptor chunk c = bytes [128 c, 128 c + 128): two per lane, one DMA of 4 bytes per lane
+  const uint16_t *dsrc = P.desc + P.units[sj.first].desc_off;  // 512-aligned
+  // descriptor chunk c = bytes [128 c, 128 c + 128): one DMA of 4 bytes per lane
   const uint64_t nchunks = (n + 127) / 128;
   uint64_t issued = 0;
   uint64_t flushed = 0;
-  for (uint64_t op = 0; op < n; op += 64) {
-    const uint64_t need = (op >> 7) + 1 < nchunks ? (op >> 7) + 1 : nchunks;
+  for (uint64_t op = 0; op < n; op += CP_STEP) {
+    const uint64_t need = (op >> 7) + 2 < nchunks ? (op >> 7) + 2 : nchunks;
     const uint64_t want = need + CP_AHEAD < nchunks ? need + CP_AHEAD : nchunks;
     while (issued < want) {
       __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint32_t *>(dsrc + issued * 128) + lane,
@@ -762,35 +810,51 @@ __global__ __launch_bounds__(64) void copy_kernel(ResolveParams P) {
       __builtin_amdgcn_s_waitcnt(0x0F70 | CP_AHEAD);
     else
       __builtin_amdgcn_s_waitcnt(0x0F70);
-    const uint64_t x = op + (uint64_t)lane;
-    const bool in = x < n;
-    const uint32_t d = in ? sh.desc[x & (CP_DESC_RING - 1)] : 0x8000u;
-    uint32_t val = d & 0xFF;
-    int32_t ptr = -1;
-    if (!(d & 0x8000u)) {
-      const uint64_t src = x - (d + 1);
-      if (src < op)
-        val = sh.ring[src & RING_MASK];
-      else
-        ptr = (int32_t)(src - op);
-    }
-    // in-step references: pointer jumping (a source lane precedes its reader)
-    while (__ballot(ptr >= 0)) {
-      const uint32_t q = ptr >= 0 ? (uint32_t)ptr : (uint32_t)lane;
-      const uint32_t v2 = bperm(val, q);
-      const int32_t p2 = (int32_t)bperm((uint32_t)ptr, q);
-      if (ptr >= 0) {
-        if (p2 < 0) {
-          val = v2;
-          ptr = -1;
-        } else {
-          ptr = p2;
+    // lane j: bytes op + 4 j .. op + 4 j + 3 (bytes past n are never flushed)
+    const uint64_t x = op + 4 * (uint64_t)lane;
+    const uint64_t dd = *reinterpret_cast<const uint64_t *>(&sh.desc[x & (CP_DESC_RING - 1)]);
+    int32_t o0, o1, o2, o3;
+    const uint32_t b0 = cp_byte(&sh, op, (uint32_t)dd & 0xFFFF, o0);
+    const uint32_t b1 = cp_byte(&sh, op, (uint32_t)(dd >> 16) & 0xFFFF, o1);
+    const uint32_t b2 = cp_byte(&sh, op, (uint32_t)(dd >> 32) & 0xFFFF, o2);
+    const uint32_t b3 = cp_byte(&sh, op, (uint32_t)(dd >> 48), o3);
+    if (__ballot((o0 | o1 | o2 | o3) >= 0) == 0) {
+      *reinterpret_cast<uint32_t *>(&sh.ring[x & RING_MASK]) = b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+    } else {
+      // a unit boundary inside this step left references into it: resolve
+      // them byte by byte (64-byte sub-steps, pointer jumping)
+      for (uint32_t sub = 0; sub < CP_STEP; sub += 64) {
+        const uint64_t y = op + sub + (uint64_t)lane;
+        const uint32_t d = y < n ? sh.desc[y & (CP_DESC_RING - 1)] : 0x8000u;  // (past n: stale)
+        int32_t off;
+        uint32_t val = cp_byte(&sh, op, d, off);
+        int32_t ptr = -1;
+        if (off >= (int32_t)(sub + lane)) off = -1;  // never forward (only stale data could say so)
+        if (off >= 0) {
+          if ((uint32_t)off < sub)
+            val = sh.ring[(op + off) & RING_MASK];  // written by an earlier sub-step
+          else
+            ptr = off - (int32_t)sub;
         }
+        while (__ballot(ptr >= 0)) {
+          const uint32_t q = ptr >= 0 ? (uint32_t)ptr : (uint32_t)lane;
+          const uint32_t v2 = bperm(val, q);
+          const int32_t p2 = (int32_t)bperm((uint32_t)ptr, q);
+          if (ptr >= 0) {
+            if (p2 < 0) {
+              val = v2;
+              ptr = -1;
+            } else {
+              ptr = p2;
+            }
+          }
+        }
+        sh.ring[y & RING_MASK] = (uint8_t)val;
+        wave_sync();
       }
     }
-    if (in) sh.ring[x & RING_MASK] = (uint8_t)val;
     wave_sync();
-    const uint64_t end = op + 64 < n ? op + 64 : n;
+    const uint64_t end = op + CP_STEP < n ? op + CP_STEP : n;
     if (end - flushed >= RS_FLUSH) {
       const uint64_t upto = flushed + RS_FLUSH;
       cp_flush(&sh, out, flushed, upto, lane);
