@@ -279,20 +279,8 @@ __device__ __forceinline__ void walk_init(Walk &w, const MatchShared *s, const D
   }
 }
 
-__device__ __forceinline__ void walk_step(Walk &w, const MatchShared *s, const DeflateParams &P, Key key) {
-  if (!w.active) return;
-  w.q -= w.link;
-  if (w.p - w.q > DF_MAXDIST) {
-    w.active = false;
-    return;
-  }
-  ++w.hops;
-  const uint32_t q = w.q;
-  w.link = s->prev[ridx(q)];
-  w.active = w.link != 0 && w.hops < w.max_hops;
-  if (w.best_len >= 4 && ld32(s, q + w.o) != w.pw) return;
-  if (((ld32(s, q) ^ w.cur) & key.kmask) != 0) return;
-  if (key.kmask2 && ((ld32(s, q + 4) ^ w.cur2) & key.kmask2) != 0) return;
+// a candidate q that passed the key checks: extend and keep the longest
+__device__ __forceinline__ void walk_extend(Walk &w, const MatchShared *s, const DeflateParams &P, uint32_t q) {
   uint32_t len = (uint32_t)P.klen;
   while (len < w.max_len) {
     const uint32_t x = ld32(s, q + len) ^ ld32(s, w.p + len);
@@ -313,6 +301,34 @@ __device__ __forceinline__ void walk_step(Walk &w, const MatchShared *s, const D
     w.o = len - 3;
     w.pw = ld32(s, w.p + w.o);
   }
+}
+
+// one hop of two walks: every LDS load of both hops is issued before any is
+// used (the walks are latency-bound pointer chases), then the checks
+__device__ __forceinline__ void walk_pair_step(Walk &a, Walk &b, const MatchShared *s, const DeflateParams &P,
+                                               Key key) {
+  const uint32_t qa = a.active ? a.q - a.link : a.q;
+  const uint32_t qb = b.active ? b.q - b.link : b.q;
+  const bool ha = a.active && a.p - qa <= (uint32_t)DF_MAXDIST;
+  const bool hb = b.active && b.p - qb <= (uint32_t)DF_MAXDIST;
+  const uint32_t la = s->prev[ridx(qa)], lb = s->prev[ridx(qb)];
+  const uint32_t oa = ld32(s, qa + a.o), ob = ld32(s, qb + b.o);
+  const uint32_t ka = ld32(s, qa), kb = ld32(s, qb);
+  const uint32_t ka2 = ld32(s, qa + 4), kb2 = ld32(s, qb + 4);
+  a.q = qa;
+  b.q = qb;
+  a.hops += ha ? 1 : 0;
+  b.hops += hb ? 1 : 0;
+  const bool ca = ha && (a.best_len < 4 || oa == a.pw) && ((ka ^ a.cur) & key.kmask) == 0 &&
+                  ((ka2 ^ a.cur2) & key.kmask2) == 0;
+  const bool cb = hb && (b.best_len < 4 || ob == b.pw) && ((kb ^ b.cur) & key.kmask) == 0 &&
+                  ((kb2 ^ b.cur2) & key.kmask2) == 0;
+  a.link = la;
+  b.link = lb;
+  a.active = ha && la != 0 && a.hops < a.max_hops;
+  b.active = hb && lb != 0 && b.hops < b.max_hops;
+  if (ca) walk_extend(a, s, P, qa);
+  if (cb) walk_extend(b, s, P, qb);
 }
 
 // finish position pb + K: near probes when the chain found nothing long
@@ -345,18 +361,12 @@ __device__ void search_sub(const MatchShared *s, const DeflateParams &P, uint32_
   Walk wa, wb;
   walk_init(wa, s, P, pb, p1, win32<16>(w), win32<20>(w), 0, 0);
   walk_init(wb, s, P, pb + 2, p1, win32<18>(w), win32<22>(w), 0, 0);
-  while (wa.active || wb.active) {
-    walk_step(wa, s, P, key);
-    walk_step(wb, s, P, key);
-  }
+  while (wa.active || wb.active) walk_pair_step(wa, wb, s, P, key);
   out[0] = walk_finish<0>(wa, P, w, c0l, c0d);
   out[2] = walk_finish<2>(wb, P, w, c2l, c2d);
   walk_init(wa, s, P, pb + 1, p1, win32<17>(w), win32<21>(w), c0l, c0d);
   walk_init(wb, s, P, pb + 3, p1, win32<19>(w), win32<23>(w), c2l, c2d);
-  while (wa.active || wb.active) {
-    walk_step(wa, s, P, key);
-    walk_step(wb, s, P, key);
-  }
+  while (wa.active || wb.active) walk_pair_step(wa, wb, s, P, key);
   out[1] = walk_finish<1>(wa, P, w, cl, cd);
   out[3] = walk_finish<3>(wb, P, w, cl, cd);
   if (pb + 4 <= p1) {
