@@ -403,9 +403,10 @@ __global__ __launch_bounds__(DF_THREADS) void match_kernel(DeflateParams P) {
   for (uint32_t i = t; i < (1u << DF_HBITS); i += DF_THREADS) s.head[i] = kNoPos;
   __syncthreads();
   uint32_t inserted = 0;  // positions [0, inserted) are in the chains
+  if (re > 0) load_sub(&s, g, 0, re < DF_SUB ? re : DF_SUB);
+  const bool g_aligned = (reinterpret_cast<uintptr_t>(g) & 3) == 0;
   for (uint32_t p0 = 0; p0 < re; p0 += DF_SUB) {
     const uint32_t p1 = (p0 + DF_SUB) < re ? (p0 + DF_SUB) : re;
-    load_sub(&s, g + p0, p0, p1 - p0);
     __syncthreads();
     uint32_t ih = p1 >= kext ? p1 - kext : 0;
     if (rend >= kext && ih > rend - kext) ih = rend - kext;
@@ -413,9 +414,21 @@ __global__ __launch_bounds__(DF_THREADS) void match_kernel(DeflateParams P) {
       chain_build(&s, inserted, ih, key);
       inserted = ih;
     }
+    // the next sub-chunk is fetched while this one is searched
+    const uint32_t n0 = p0 + DF_SUB;
+    const bool fast = g_aligned && n0 + DF_SUB <= re;
+    uint32_t nv = 0;
+    if (fast) nv = reinterpret_cast<const uint32_t *>(g + n0)[t];
     // res is indexed by input position: rel r <-> input h_lo + r - halo
     if (p0 >= rs) search_sub(&s, P, p0, p1, key, P.res + (h_lo + p0 - P.halo));
     __syncthreads();
+    if (fast) {
+      const uint32_t k0 = ridx(n0);
+      s.ring[(k0 >> 2) + t] = nv;
+      if (k0 == 0 && t < 16) s.ring[DF_RING / 4 + t] = nv;
+    } else if (n0 < re) {
+      load_sub(&s, g + n0, n0, (re - n0) < DF_SUB ? (re - n0) : DF_SUB);
+    }
   }
 }
 
