@@ -38,6 +38,10 @@
 
 namespace zt {
 
+#ifdef ZT_DF_COUNT
+__device__ unsigned long long g_df_count[4];  // debug: pair steps (per wave), lane hops, extends
+#endif
+
 constexpr int DF_BLOCK = 32768;
 constexpr int DF_SUB = 4096;
 constexpr int DF_RING = 32768;  // power of two: ring index = rel & (DF_RING - 1)
@@ -281,6 +285,9 @@ __device__ __forceinline__ void walk_init(Walk &w, const MatchShared *s, const D
 
 // a candidate q that passed the key checks: extend and keep the longest
 __device__ __forceinline__ void walk_extend(Walk &w, const MatchShared *s, const DeflateParams &P, uint32_t q) {
+#ifdef ZT_DF_COUNT
+  atomicAdd(&g_df_count[2], 1ull);
+#endif
   uint32_t len = (uint32_t)P.klen;
   while (len < w.max_len) {
     const uint32_t x = ld32(s, q + len) ^ ld32(s, w.p + len);
@@ -319,6 +326,10 @@ __device__ __forceinline__ void walk_pair_step(Walk &a, Walk &b, const MatchShar
   b.q = qb;
   a.hops += ha ? 1 : 0;
   b.hops += hb ? 1 : 0;
+#ifdef ZT_DF_COUNT
+  if ((threadIdx.x & 63) == 0) atomicAdd(&g_df_count[0], 1ull);
+  atomicAdd(&g_df_count[1], (unsigned long long)(ha ? 1 : 0) + (hb ? 1 : 0));
+#endif
   const bool ca = ha && (a.best_len < 4 || oa == a.pw) && ((ka ^ a.cur) & key.kmask) == 0 &&
                   ((ka2 ^ a.cur2) & key.kmask2) == 0;
   const bool cb = hb && (b.best_len < 4 || ob == b.pw) && ((kb ^ b.cur) & key.kmask) == 0 &&
@@ -1258,6 +1269,15 @@ int deflate_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t halo, in
   *out_len = total;
   return ZT_OK;
 }
+
+#ifdef ZT_DF_COUNT
+extern "C" int zt_debug_df_count(unsigned long long *out) {
+  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_df_count), sizeof(unsigned long long) * 4);
+  unsigned long long z[4] = {};
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_df_count), z, sizeof z);
+  return 0;
+}
+#endif
 
 size_t deflate_scratch_bytes(const DeviceCtx *c, size_t n) {
   DeflateGeom G;
