@@ -1,1 +1,10 @@
-ZT_LIB=$PWD/zlib.ts_amd/libzt_cnt.so timeout -k 10 300 python tools/df_count.py wordsalad structured xorshift32 2>&1 | grep -v amdgpu.ids
+set -e
+export TMPDIR=/tmp
+rocprofv3 -L > gpurun_out/counters.txt 2>&1 || true
+grep -E "FETCH_SIZE|WRITE_SIZE|TCC_EA0_RDREQ|TCC_EA0_WRREQ|TCC_BUBBLE" gpurun_out/counters.txt | head -20
+cd /tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -f csv -d $GRAFT_REPO_ROOT/gpurun_out/pmcf -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 0 --no-cpu-baseline > /dev/null 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -f csv -d $GRAFT_REPO_ROOT/gpurun_out/pmcw -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 0 --no-cpu-baseline > /dev/null 2>&1
+cd $GRAFT_REPO_ROOT
+python3 tools/pmc_summ.py gpurun_out/pmcf
+python3 tools/pmc_summ.py gpurun_out/pmcw
