@@ -1,10 +1,6 @@
 set -e
+timeout -k 10 600 python -m pytest tests -m gpu -x -q -k deflate > gpurun_out/t2.log 2>&1 || { tail -40 gpurun_out/t2.log; exit 1; }
+tail -1 gpurun_out/t2.log
 export TMPDIR=/tmp
-rocprofv3 -L > gpurun_out/counters.txt 2>&1 || true
-grep -E "FETCH_SIZE|WRITE_SIZE|TCC_EA0_RDREQ|TCC_EA0_WRREQ|TCC_BUBBLE" gpurun_out/counters.txt | head -20
-cd /tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -f csv -d $GRAFT_REPO_ROOT/gpurun_out/pmcf -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 0 --no-cpu-baseline > /dev/null 2>&1
-timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -f csv -d $GRAFT_REPO_ROOT/gpurun_out/pmcw -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 0 --no-cpu-baseline > /dev/null 2>&1
-cd $GRAFT_REPO_ROOT
-python3 tools/pmc_summ.py gpurun_out/pmcf
-python3 tools/pmc_summ.py gpurun_out/pmcw
+cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d $GRAFT_REPO_ROOT/gpurun_out/p6 -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/p6.log 2>&1
+cd $GRAFT_REPO_ROOT; cut -d, -f1-4 gpurun_out/p6/run_kernel_stats.csv | cut -c1-120 | head -9
