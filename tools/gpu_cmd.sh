@@ -1,6 +1,5 @@
 set -e
 timeout -k 10 600 python -m pytest tests -m gpu -x -q -k deflate > gpurun_out/t2.log 2>&1 || { tail -40 gpurun_out/t2.log; exit 1; }
 tail -1 gpurun_out/t2.log
-export TMPDIR=/tmp
-cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d $GRAFT_REPO_ROOT/gpurun_out/p6 -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/p6.log 2>&1
-cd $GRAFT_REPO_ROOT; cut -d, -f1-4 gpurun_out/p6/run_kernel_stats.csv | cut -c1-120 | head -9
+timeout -k 10 600 python tools/df_sweep.py wordsalad 32,128,1,128,8,16,16 2>&1 | grep -v amdgpu.ids
+timeout -k 10 600 python tools/df_sweep.py structured 32,128,1,128,8,16,16 2>&1 | grep -v amdgpu.ids

@@ -289,7 +289,21 @@ __device__ __forceinline__ void walk_extend(Walk &w, const MatchShared *s, const
   atomicAdd(&g_df_count[2], 1ull);
 #endif
   uint32_t len = (uint32_t)P.klen;
-  while (len < w.max_len) {
+  {
+    // the next 16 bytes in one round of loads (most matches end there)
+    const uint32_t x0 = ld32(s, q + len) ^ ld32(s, w.p + len);
+    const uint32_t x1 = ld32(s, q + len + 4) ^ ld32(s, w.p + len + 4);
+    const uint32_t x2 = ld32(s, q + len + 8) ^ ld32(s, w.p + len + 8);
+    const uint32_t x3 = ld32(s, q + len + 12) ^ ld32(s, w.p + len + 12);
+    if (x0) len += (uint32_t)(__ffs(x0) - 1) >> 3;
+    else if (x1) len += 4 + ((uint32_t)(__ffs(x1) - 1) >> 3);
+    else if (x2) len += 8 + ((uint32_t)(__ffs(x2) - 1) >> 3);
+    else if (x3) len += 12 + ((uint32_t)(__ffs(x3) - 1) >> 3);
+    else len += 16;
+  }
+  const bool more = len == (uint32_t)P.klen + 16;
+  while (more && len < w.max_len) {
+    // all 16 matched: continue 4 bytes at a time
     const uint32_t x = ld32(s, q + len) ^ ld32(s, w.p + len);
     if (x) {
       len += (uint32_t)(__ffs(x) - 1) >> 3;
