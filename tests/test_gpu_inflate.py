@@ -166,3 +166,42 @@ def test_errors(zt):
         with pytest.raises(ztamd.ZtError) as ei:
             zt.inflate_raw(s)
         assert ei.value.msg == msg
+
+
+@pytest.mark.parametrize("step", [10007, 4093, 65521])
+@pytest.mark.parametrize("mode", ["sync", "full"])
+def test_two_phase_unaligned_units(zt, oracle, step, mode):
+    """zlib sync / full flushes at arbitrary offsets give sync points whose
+    units are not aligned to the 256-byte copy steps: references that cross a
+    unit boundary inside a step go through copy_kernel's pointer jumping."""
+    d = oracle.gen("wordsalad", step, 600000) + oracle.gen("structured", step, 300000) + b"ab" * 50000
+    c = zlib.compressobj(6, zlib.DEFLATED, -15)
+    flush = zlib.Z_SYNC_FLUSH if mode == "sync" else zlib.Z_FULL_FLUSH
+    parts = []
+    for o in range(0, len(d), step):
+        parts.append(c.compress(d[o:o + step]) + c.flush(flush))
+    parts.append(c.flush())
+    s = b"".join(parts)
+    zt.timing_enable(True)
+    out, ip = zt.inflate_raw(s)
+    t = zt.timing_read()
+    zt.timing_enable(False)
+    assert out == d and ip == len(s)
+    assert t["inflate_toks"] == 1, "the two-phase inflate did not run"
+
+
+def test_two_phase_block_shapes(zt, oracle):
+    """Fixed-code blocks, tiny blocks, long codes and stored blocks between
+    sync points (zlib strategies and levels)."""
+    d = b"".join(oracle.gen(k, 31 + i, 70000 + 977 * i) for i, k in
+                 enumerate(["wordsalad", "xorshift32", "structured", "wordsalad"]))
+    for level, strategy in [(1, zlib.Z_FIXED), (9, zlib.Z_DEFAULT_STRATEGY), (6, zlib.Z_HUFFMAN_ONLY),
+                            (0, zlib.Z_DEFAULT_STRATEGY), (6, zlib.Z_RLE)]:
+        c = zlib.compressobj(level, zlib.DEFLATED, -15, 9, strategy)
+        parts = []
+        for o in range(0, len(d), 20000):
+            parts.append(c.compress(d[o:o + 20000]) + c.flush(zlib.Z_SYNC_FLUSH))
+        parts.append(c.flush())
+        s = b"".join(parts)
+        out, ip = zt.inflate_raw(s)
+        assert out == d and ip == len(s), (level, strategy)

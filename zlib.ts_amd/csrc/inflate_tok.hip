@@ -818,7 +818,7 @@ __global__ __launch_bounds__(64) void copy_kernel(ResolveParams P) {
     const uint32_t b1 = cp_byte(&sh, op, (uint32_t)(dd >> 16) & 0xFFFF, o1);
     const uint32_t b2 = cp_byte(&sh, op, (uint32_t)(dd >> 32) & 0xFFFF, o2);
     const uint32_t b3 = cp_byte(&sh, op, (uint32_t)(dd >> 48), o3);
-    if (__ballot((o0 | o1 | o2 | o3) >= 0) == 0) {
+    if (__ballot(o0 >= 0 || o1 >= 0 || o2 >= 0 || o3 >= 0) == 0) {
       *reinterpret_cast<uint32_t *>(&sh.ring[x & RING_MASK]) = b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
     } else {
       // a unit boundary inside this step left references into it: resolve
