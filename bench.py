@@ -73,6 +73,21 @@ def cpu_baseline(d_in, level, zt):
     }, ratios
 
 
+def pmc_traffic(kernel, n):
+    """HBM bytes per launch of `kernel` measured by rocprofv3 PMC passes
+    (FETCH_SIZE x2 + WRITE_SIZE, tools/pmc_traffic.py) on this workload, or
+    None when no measurement for this size is committed."""
+    path = os.path.join(HERE, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            k = json.load(f)["kernels"][kernel]
+    except (OSError, KeyError, ValueError):
+        return None
+    if n != 1 << 30:
+        return None
+    return int(k["traffic_bytes"])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -168,7 +183,7 @@ def main():
         "inflate_GiBps": round(n / (inf_ms * 1e-3) / 2**30, 3) if inf_ms else None,
         "roofline": {"bound": "hbm", "kernel": "match_kernel", "achieved": round(achieved, 3),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
-                     "traffic": None},
+                     "traffic": pmc_traffic("match_kernel", n)},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and n >= 3 * WINDOW:
         cb, ratios = cpu_baseline(d_in, args.level, zt)
