@@ -487,13 +487,60 @@ __device__ __forceinline__ void wsync() {
 
 // freq[0..n) -> len[0..n), limited to `limit` bits.  Always produces a complete
 // code with >= 2 symbols (zlib's rule), forcing symbols 0/1 in when needed.
+// ascending bitonic sort of 64 * R keys held R per lane (key index lane * R + r):
+// partners inside a lane are register swaps, others one cross-lane shuffle
+template <int R>
+__device__ __forceinline__ void reg_bitonic(uint32_t (&key)[R], int lane) {
+  constexpr int N = 64 * R;
+#pragma unroll
+  for (int k = 2; k <= N; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      if (j < R) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          if ((r & j) == 0) {
+            const uint32_t i = (uint32_t)lane * R + r;
+            const bool up = (i & k) == 0;
+            const uint32_t a = key[r], b = key[r | j];
+            const bool sw = (a > b) == up;
+            key[r] = sw ? b : a;
+            key[r | j] = sw ? a : b;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const uint32_t other = (uint32_t)__shfl_xor((int)key[r], j / R, 64);
+          const uint32_t i = (uint32_t)lane * R + r;
+          const bool up = (i & k) == 0;
+          const bool lower = (i & j) == 0;
+          const uint32_t mn = key[r] < other ? key[r] : other, mx = key[r] < other ? other : key[r];
+          key[r] = (lower == up) ? mn : mx;
+        }
+      }
+    }
+  }
+}
+
+// keys (freq << 9 | symbol, or ~0 for unused) sorted ascending into h.key[0..)
+template <int R>
+__device__ __forceinline__ void sort_keys(HufScratch &h, const uint32_t *freq_in, int n, int lane) {
+  uint32_t key[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int i = lane * R + r;
+    const uint32_t f = i < n ? freq_in[i] : 0u;
+    key[r] = (i < n && f) ? ((f << 9) | (uint32_t)i) : 0xFFFFFFFFu;
+  }
+  reg_bitonic<R>(key, lane);
+#pragma unroll
+  for (int r = 0; r < R; ++r) h.key[lane * R + r] = key[r];
+}
+
 __device__ void huff_lengths(BlockShared *s, const uint32_t *freq_in, int n, int limit, uint8_t *len_out) {
   const int lane = threadIdx.x & 63;
   HufScratch &h = s->huf;
-  for (int i = lane; i < 512; i += 64) {
-    uint32_t f = i < n ? freq_in[i] : 0;
-    h.key[i] = (i < n && f) ? ((f << 9) | (uint32_t)i) : 0xFFFFFFFFu;
-  }
   for (int i = lane; i < n; i += 64) len_out[i] = 0;
   wsync();
   uint32_t m = 0;
@@ -517,23 +564,12 @@ __device__ void huff_lengths(BlockShared *s, const uint32_t *freq_in, int n, int
     wsync();
     return;
   }
-  // bitonic sort of 512 keys
-  for (int k = 2; k <= 512; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = lane; i < 512; i += 64) {
-        int ixj = i ^ j;
-        if (ixj > i) {
-          uint32_t a = h.key[i], b = h.key[ixj];
-          bool up = (i & k) == 0;
-          if ((a > b) == up) {
-            h.key[i] = b;
-            h.key[ixj] = a;
-          }
-        }
-      }
-      wsync();
-    }
-  }
+  // sort by (frequency, symbol) in registers
+  if (n <= 64)
+    sort_keys<1>(h, freq_in, n, lane);
+  else
+    sort_keys<8>(h, freq_in, n, lane);
+  wsync();
   if (lane == 0) {
     uint32_t *A = h.a;
     for (uint32_t i = 0; i < m; ++i) A[i] = h.key[i] >> 9;
