@@ -1,0 +1,13 @@
+#!/bin/bash
+# Build libzt.so with extra compile flags into build/var_NAME/ (tuning experiments;
+# load it with ZT_LIB=...).   usage: tools/build_variant.sh NAME FLAGS...
+set -e
+NAME=$1; shift
+cd "$(dirname "$0")/../zlib.ts_amd"
+OUT=build/var_$NAME; mkdir -p $OUT
+for f in csrc/*.hip csrc/*.cpp; do
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-function "$@" -c -o $OUT/$(basename $f).o $f &
+done
+wait
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -shared -o $OUT/libzt.so $OUT/*.o
+echo built $OUT/libzt.so

@@ -38,6 +38,12 @@
 
 namespace zt {
 
+#ifdef ZT_DF_TIME
+__device__ unsigned long long g_df_time[4];  // debug: cycles (thread 0 of each workgroup) in phases
+#define DF_T(v) v = __builtin_readcyclecounter()
+#else
+#define DF_T(v) (void)0
+#endif
 #ifdef ZT_DF_COUNT
 __device__ unsigned long long g_df_count[4];  // debug: pair steps (per wave), lane hops, extends
 #endif
@@ -46,7 +52,10 @@ constexpr int DF_BLOCK = 32768;
 constexpr int DF_SUB = 4096;
 constexpr int DF_RING = 32768;  // power of two: ring index = rel & (DF_RING - 1)
 constexpr int DF_SLOT = DF_BLOCK + DF_BLOCK / 8 + 1024;  // per-block slot: fits a forced fixed-code block
-constexpr int DF_HBITS = 13;
+#ifndef ZT_DF_HBITS
+#define ZT_DF_HBITS 14
+#endif
+constexpr int DF_HBITS = ZT_DF_HBITS;
 constexpr int DF_THREADS = 1024;
 // the ring holds [p1 - DF_RING, p1) while sub-chunk [p0, p1) is searched;
 // a super-chunk loads DF_HIST bytes of history first (whole sub-chunks)
@@ -55,7 +64,8 @@ constexpr int DF_MAXDIST = DF_HIST - 64;      // 28608
 constexpr int ENC_THREADS = 256;
 // Independent segments of 1 MiB: restart points for segment-parallel inflate
 constexpr uint32_t kRestartBlocks = 32;
-constexpr uint32_t kNoPos = 0x80000000u;  // empty head entry (p - kNoPos is never a valid distance)
+// empty head entry: p - kNoHead (mod 2^16) exceeds DF_MAXDIST for p < 25536
+constexpr uint16_t kNoHead = (uint16_t)(65536 - 40000);
 
 struct BlockPlan;
 
@@ -76,6 +86,7 @@ struct DeflateParams {
   int klen;             // chain key length: 3, 4, 6 or 8 bytes (shorter matches come from near probes)
   int probe;            // near distances 1..probe checked for matches shorter than klen
   int ctype;            // 1: fixed codes only; 2: best of dynamic/fixed/stored
+  int opt;              // cost-based parse (optparse_kernel) between match and block kernels
   uint32_t *res;        // n: per-position match, then (in place) per-block tokens
   uint8_t *slots;       // nblocks x DF_SLOT
   uint32_t *slot_len;   // nblocks
@@ -126,8 +137,10 @@ __device__ __forceinline__ uint32_t len_sym(uint32_t L) {  // 0..28 (symbol - 25
 struct MatchShared {
   uint32_t ring[DF_RING / 4 + 16];  // data ring + 64-byte mirror of its start
   uint16_t prev[DF_RING];           // relative chain links (0 = none)
-  uint32_t head[1 << DF_HBITS];     // newest position (rel) per hash, or kNoPos
+  uint16_t head[1 << DF_HBITS];     // newest position (rel) per hash, mod 2^16 (see chain_build)
   uint16_t hbuf[DF_SUB + 64];       // hashes of the positions being linked
+  uint32_t linked;                  // positions below are linked (chain_link -> searching waves)
+  uint32_t work;                    // next super-step of 256 positions to search
 };
 
 __device__ __forceinline__ uint32_t ridx(uint32_t rel) { return rel & (DF_RING - 1); }
@@ -168,11 +181,15 @@ __device__ void load_sub(MatchShared *s, const uint8_t *g, uint32_t rel0, uint32
   }
 }
 
-// chain links for positions [lo, hi) (rel coords, hi - lo <= DF_SUB + 3)
-__device__ void chain_build(MatchShared *s, uint32_t lo, uint32_t hi, Key key) {
+// chain links for positions [lo, hi) (rel coords, hi - lo <= DF_SUB + 3), in two parts:
+// chain_hash (all waves): hashes, and each position's predecessor inside its
+//   step of 64 by ballot peer masks (bit 15 of prev: last of its hash in the step)
+// chain_link (one wave): links the step leaders to the head table in position
+//   order, publishing its progress in s->linked while the other waves search
+//   the positions already linked (match_kernel)
+__device__ void chain_hash(MatchShared *s, uint32_t lo, uint32_t hi, Key key) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t nsteps = (hi - lo + 63) / 64;
-  // (1) hashes and in-step predecessors, all waves
   for (uint32_t st = wave; st < nsteps; st += DF_THREADS / 64) {
     const uint32_t p = lo + st * 64 + lane;
     const bool valid = p < hi;
@@ -191,25 +208,48 @@ __device__ void chain_build(MatchShared *s, uint32_t lo, uint32_t hi, Key key) {
       s->hbuf[p - lo] = (uint16_t)h;
     }
   }
-  __syncthreads();
-  // (2) one wave links the step leaders to the head table, in position order
-  if (wave == 0) {
-    for (uint32_t st = 0; st < nsteps; ++st) {
-      const uint32_t p = lo + st * 64 + lane;
-      if (p < hi) {
-        const uint32_t e = s->prev[ridx(p)];
-        const uint32_t h = s->hbuf[p - lo];
-        uint32_t link = e & 0x7F;
-        if (link == 0) {
-          const uint32_t d = p - s->head[h];
-          link = d <= DF_MAXDIST ? d : 0;
-        }
-        s->prev[ridx(p)] = (uint16_t)link;
-        if (e & 0x8000) s->head[h] = p;
+}
+
+constexpr int CB_PF = 4;  // steps whose (prev, hash) pairs are read ahead; progress published per CB_PF steps
+__device__ void chain_link(MatchShared *s, uint32_t lo, uint32_t hi) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t nsteps = (hi - lo + 63) / 64;
+  uint32_t eh[CB_PF];  // prev | hash << 16 of step st + j
+  // branch-free reads: a branch join would make the compiler wait for every
+  // LDS load in flight
+  auto fetch = [&](uint32_t st) -> uint32_t {
+    const uint32_t p = lo + st * 64 + lane;
+    const uint32_t pc = p < hi ? p : lo;
+    const uint32_t v = (uint32_t)s->prev[ridx(pc)] | ((uint32_t)s->hbuf[pc - lo] << 16);
+    return p < hi ? v : 1u;
+  };
+#pragma unroll
+  for (int j = 0; j < CB_PF; ++j) eh[j] = fetch(j);
+  for (uint32_t sb = 0; sb < nsteps; sb += CB_PF) {
+#pragma unroll
+    for (int j = 0; j < CB_PF; ++j) {
+      const uint32_t st = sb + j;
+      if (st < nsteps) {
+        const uint32_t p = lo + st * 64 + lane;
+        const uint32_t e = eh[j] & 0xFFFF, h = eh[j] >> 16;
+        // the head read is issued before the read-ahead, so waiting for it
+        // leaves the read-ahead in flight
+        const uint32_t hd = s->head[h];
+        eh[j] = fetch(st + CB_PF);
+        // heads are kept mod 2^16: an entry 2^16 or more positions old
+        // aliases a recent position of another hash, which only costs a
+        // hop (every candidate is verified byte by byte); d <= p keeps
+        // the link inside the loaded range
+        const uint32_t d = (uint16_t)(p - hd);
+        const uint32_t link = (e & 0x7F) ? (e & 0x7F) : (d <= DF_MAXDIST && d <= p ? d : 0u);
+        if (p < hi) s->prev[ridx(p)] = (uint16_t)link;
+        if (p < hi && (e & 0x8000)) s->head[h] = (uint16_t)p;
       }
     }
+    const uint32_t done = lo + (sb + CB_PF) * 64;
+    if (lane == 0)
+      __hip_atomic_store(&s->linked, done < hi ? done : hi, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
-  __syncthreads();
 }
 
 // 4 bytes at byte x of a register window (x a compile-time constant after unrolling)
@@ -369,11 +409,9 @@ __device__ __forceinline__ uint32_t walk_finish(const Walk &w, const DeflatePara
   return best_len >= 3 ? (best_len << 16) | best_dist : 0u;
 }
 
-// longest match for positions [p0, p1) (4 per thread) -> res_out[p - p0]
-__device__ void search_sub(const MatchShared *s, const DeflateParams &P, uint32_t p0, uint32_t p1, Key key,
-                           uint32_t *res_out) {
-  const uint32_t t = threadIdx.x;
-  const uint32_t pb = p0 + t * 4;
+// longest match for positions [pb, pb + 4) of the sub-chunk [p0, p1) -> res_out[p - p0]
+__device__ void search_quad(const MatchShared *s, const DeflateParams &P, uint32_t pb, uint32_t p0, uint32_t p1,
+                            Key key, uint32_t *res_out) {
   if (pb >= p1) return;
   // bytes [pb - 16, pb + 16) (pb is a multiple of 4; before rel 0 the words
   // are never used: near distances stay <= p)
@@ -425,7 +463,7 @@ __global__ __launch_bounds__(DF_THREADS) void match_kernel(DeflateParams P) {
   key.kmask2 = P.klen >= 8 ? 0xFFFFFFFFu : P.klen == 6 ? 0xFFFFu : P.klen == 5 ? 0xFFu : 0u;
   const uint32_t kext = (uint32_t)P.klen - 1;  // a key at p needs bytes up to p + kext
 
-  for (uint32_t i = t; i < (1u << DF_HBITS); i += DF_THREADS) s.head[i] = kNoPos;
+  for (uint32_t i = t; i < (1u << DF_HBITS); i += DF_THREADS) s.head[i] = kNoHead;
   __syncthreads();
   uint32_t inserted = 0;  // positions [0, inserted) are in the chains
   if (re > 0) load_sub(&s, g, 0, re < DF_SUB ? re : DF_SUB);
@@ -433,20 +471,53 @@ __global__ __launch_bounds__(DF_THREADS) void match_kernel(DeflateParams P) {
   for (uint32_t p0 = 0; p0 < re; p0 += DF_SUB) {
     const uint32_t p1 = (p0 + DF_SUB) < re ? (p0 + DF_SUB) : re;
     __syncthreads();
+    uint64_t t0, t1, t2, t3;
+    DF_T(t0);
     uint32_t ih = p1 >= kext ? p1 - kext : 0;
     if (rend >= kext && ih > rend - kext) ih = rend - kext;
-    if (ih > inserted) {
-      chain_build(&s, inserted, ih, key);
-      inserted = ih;
+    const bool link = ih > inserted;
+    if (link) chain_hash(&s, inserted, ih, key);
+    if (t == 0) {
+      s.linked = link ? inserted : ih;
+      s.work = 0;
     }
     // the next sub-chunk is fetched while this one is searched
     const uint32_t n0 = p0 + DF_SUB;
     const bool fast = g_aligned && n0 + DF_SUB <= re;
     uint32_t nv = 0;
     if (fast) nv = reinterpret_cast<const uint32_t *>(g + n0)[t];
-    // res is indexed by input position: rel r <-> input h_lo + r - halo
-    if (p0 >= rs) search_sub(&s, P, p0, p1, key, P.res + (h_lo + p0 - P.halo));
     __syncthreads();
+    DF_T(t1);
+    // wave 0 links the chains step by step; every wave (wave 0 once done)
+    // takes super-steps of 256 positions in order and searches them as soon
+    // as their links are final (positions only read links of older ones)
+    if (t < 64 && link) chain_link(&s, inserted, ih);
+    inserted = link ? ih : inserted;
+    if (p0 >= rs) {
+      const uint32_t nss = (p1 - p0 + 255) / 256;
+      uint32_t *res_out = P.res + (h_lo + p0 - P.halo);  // res[input pos]: rel r <-> input h_lo + r - halo
+      for (;;) {
+        uint32_t ss = 0;
+        if ((t & 63) == 0) ss = atomicAdd(&s.work, 1u);
+        ss = (uint32_t)__shfl((int)ss, 0, 64);
+        if (ss >= nss) break;
+        const uint32_t need = (p0 + 256 * (ss + 1)) < ih ? (p0 + 256 * (ss + 1)) : ih;
+        while (__hip_atomic_load(&s.linked, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
+          __builtin_amdgcn_s_sleep(1);
+        search_quad(&s, P, p0 + 256 * ss + 4 * (t & 63), p0, p1, key, res_out);
+      }
+    }
+    DF_T(t2);
+    __syncthreads();
+    DF_T(t3);
+#ifdef ZT_DF_TIME
+    if (t == 0) {
+      atomicAdd(&g_df_time[0], (unsigned long long)(t1 - t0));
+      atomicAdd(&g_df_time[1], (unsigned long long)(t2 - t1));
+      atomicAdd(&g_df_time[2], (unsigned long long)(t3 - t2));
+      atomicAdd(&g_df_time[3], 1ull);
+    }
+#endif
     if (fast) {
       const uint32_t k0 = ridx(n0);
       s.ring[(k0 >> 2) + t] = nv;
@@ -700,27 +771,41 @@ struct HdrOut {
 };
 
 // parse (pointer doubling over 64-position windows) -> tokens over res, histograms
-__device__ uint32_t parse_block(BlockShared *s, const DeflateParams &P, uint32_t *r_blk, const uint8_t *data,
-                                uint32_t len) {
+// (WRITE = false: histograms of the greedy parse only, res untouched)
+constexpr int PB_PF = 6;  // parse windows prefetched
+template <bool WRITE, class S>
+__device__ uint32_t parse_block(S *s, const DeflateParams &P, uint32_t *r_blk, const uint8_t *data, uint32_t len) {
   const int lane = threadIdx.x & 63;
   uint32_t entry = 0;  // first path position relative to the current window
   uint32_t ntok = 0;
-  // software pipeline: the next windows' loads are in flight while one is parsed
-  uint32_t r_nx = (uint32_t)lane < len ? r_blk[lane] : 0u;
-  uint32_t r_nx2 = 64u + lane < len ? r_blk[64 + lane] : 0u;  // also the lazy look-ahead
-  uint32_t b_nx = (uint32_t)lane < len ? data[lane] : 0u;
-  for (uint32_t w0 = 0; w0 < len; w0 += 64) {
-    const uint32_t r = r_nx, r_next = r_nx2, byte = b_nx;
-    r_nx = r_next;
-    r_nx2 = w0 + 128 + lane < len ? r_blk[w0 + 128 + lane] : 0u;
-    b_nx = w0 + 64 + lane < len ? data[w0 + 64 + lane] : 0u;
+  // software pipeline: PB_PF windows' loads are in flight while one is parsed
+  // (rq[j] / bq[j] hold window w0 + 64 j; rq[j + 1] is the lazy look-ahead)
+  uint32_t rq[PB_PF], bq[PB_PF];
+#pragma unroll
+  for (int j = 0; j < PB_PF; ++j) {
+    const uint32_t p = 64u * j + lane;
+    rq[j] = p < len ? r_blk[p] : 0u;
+    bq[j] = p < len ? data[p] : 0u;
+  }
+  for (uint32_t wb = 0; wb < len; wb += 64 * PB_PF) {
+#pragma unroll
+    for (int j = 0; j < PB_PF; ++j) {
+    const uint32_t w0 = wb + 64u * j;
+    if (w0 >= len) break;
+    const uint32_t r = rq[j], byte = bq[j];
+    {
+      const uint32_t p = w0 + 64u * PB_PF + lane;
+      rq[j] = p < len ? r_blk[p] : 0u;
+      bq[j] = p < len ? data[p] : 0u;
+    }
+    const uint32_t r_next = rq[(j + 1) % PB_PF];
     if (entry >= 64) {
       entry -= 64;
       continue;
     }
     const uint32_t i = w0 + lane;
     uint32_t L = r >> 16;
-    if (P.lazy) {
+    if (P.lazy && !P.opt) {
       // one-step lazy: a longer match at i + 1 defers this one
       uint32_t nb = (uint32_t)__shfl_down((int)r, 1, 64) >> 16;
       const uint32_t first_next = (uint32_t)__shfl((int)r_next, 0, 64) >> 16;
@@ -759,12 +844,234 @@ __device__ uint32_t parse_block(BlockShared *s, const DeflateParams &P, uint32_t
         token = byte;
         atomicAdd(&s->lit_hist[token], 1u);
       }
-      r_blk[ntok + __popcll(path & lanemask_lt(lane))] = token;
+      if (WRITE) r_blk[ntok + __popcll(path & lanemask_lt(lane))] = token;
     }
     ntok += __popcll(path);
     entry = exit - 64;
+    }
   }
   return ntok;
+}
+
+// ================================ 1b. optparse_kernel ================================
+// Cost-based parse of one 32 KiB block per wavefront (levels with opt = 1).
+// price_kernel: the greedy parse of the block gives symbol statistics; their
+// entropy gives a price per literal, length and distance symbol (1/8 bit
+// units, <= 15 bits per symbol).  optparse_kernel:  Each lane then runs a backward shortest-path DP over its own
+// 512-position segment (plus 128 positions of the next segment, where paths
+// have converged): C[i] = min(lit(i) + C[i+1], min_l len(l) + dist(D_i) +
+// C[i+l]) over l in 3..min(L_i, 16) and l = L_i, for the longest match
+// (L_i, D_i) the match kernel found at i.  The chosen length is written over
+// res[i] (0 = literal), so the block kernel's parse follows the DP's path.
+// Every value left in res is a valid (shorter or equal) match, so the stream
+// stays correct whatever the cost model says.
+// C is kept modulo 2^16 in a 260-row LDS ring per lane (row = step mod 260,
+// all lanes on the same row at the same step, so reads of one length l hit
+// distinct banks): differences over <= 258 positions stay below 2^15.
+typedef unsigned int op_u32x4 __attribute__((ext_vector_type(4)));
+constexpr int OP_SEG = 512;
+constexpr int OP_OV = 128;
+constexpr int OP_RING = 260;
+constexpr int OP_SHORT = 16;
+constexpr int OP_PF = 4;      // groups of 16 positions prefetched per lane  // every cut length 3..OP_SHORT is tried, longer ones only at L
+
+// prices of one block, in 1/8 bits (price_kernel -> optparse_kernel), kept at
+// the start of the block's slot until block_kernel writes its header there
+struct BlockPrices {
+  uint8_t litc[256];
+  uint8_t lenc[260];  // by match length (3..258), extra bits included
+  uint8_t distc[32];  // by distance symbol, extra bits included
+  uint32_t any_match;
+};
+
+struct PriceShared {
+  uint32_t lit_hist[288];
+  uint32_t dist_hist[32];
+};
+
+__device__ __forceinline__ uint32_t op_price(uint32_t f, float inv_total) {
+  // -log2((f + 0.5) / total) in 1/8 bits, clamped to [1, 15] bits
+  float b = -__log2f(((float)f + 0.5f) * inv_total) * 8.0f;
+  int c = (int)(b + 0.5f);
+  return (uint32_t)(c < 8 ? 8 : c > 120 ? 120 : c);
+}
+
+// greedy parse statistics -> prices (one wave per block, small LDS: many waves per CU)
+__global__ __launch_bounds__(64) void price_kernel(DeflateParams P) {
+  __shared__ PriceShared sh;
+  PriceShared *s = &sh;
+  const int lane = threadIdx.x;
+  const uint32_t blk = blockIdx.x;
+  const uint64_t lo = (uint64_t)blk * DF_BLOCK;
+  const uint64_t n = P.end - P.halo;
+  const uint32_t blen = (uint32_t)((n - lo) < DF_BLOCK ? (n - lo) : DF_BLOCK);
+  for (int i = lane; i < 288; i += 64) s->lit_hist[i] = 0;
+  if (lane < 32) s->dist_hist[lane] = 0;
+  wsync();
+  parse_block<false>(s, P, P.res + lo, P.base + P.halo + lo, blen);
+  wsync();
+  BlockPrices *bp = reinterpret_cast<BlockPrices *>(P.slots + (size_t)blk * DF_SLOT);
+  float tl = 0.f, td = 0.f;
+  for (int i = lane; i < 286; i += 64) tl += (float)s->lit_hist[i] + 0.5f;
+  uint32_t dsum = lane < 30 ? s->dist_hist[lane] : 0u;
+  if (lane < 30) td = (float)dsum + 0.5f;
+  for (int off = 32; off; off >>= 1) {
+    tl += __shfl_xor(tl, off, 64);
+    td += __shfl_xor(td, off, 64);
+    dsum += __shfl_xor(dsum, off, 64);
+  }
+  const float il = 1.0f / tl, id = 1.0f / td;
+  for (int i = lane; i < 256; i += 64) bp->litc[i] = (uint8_t)op_price(s->lit_hist[i], il);
+  if (lane < 32) bp->distc[lane] = lane < 30 ? (uint8_t)(op_price(s->dist_hist[lane], id) + 8 * dist_extra(lane)) : 255;
+  for (int l = lane; l < 260; l += 64) {
+    uint8_t v = 255;
+    if (l >= 3 && l <= 258) {
+      const uint32_t ls = len_sym(l);
+      v = (uint8_t)(op_price(s->lit_hist[257 + ls], il) + 8 * len_extra(ls));
+    }
+    bp->lenc[l] = v;
+  }
+  if (lane == 0) bp->any_match = dsum;
+}
+
+struct OptShared {
+  BlockPrices pr;
+  uint16_t ring[OP_RING][64];
+};
+
+__device__ __forceinline__ uint32_t op_min3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_min3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+__global__ __launch_bounds__(64) void optparse_kernel(DeflateParams P) {
+  __shared__ OptShared sh;
+  OptShared *s = &sh;
+  const int lane = threadIdx.x;
+  const uint32_t blk = blockIdx.x;
+  const uint64_t lo = (uint64_t)blk * DF_BLOCK;
+  const uint64_t n = P.end - P.halo;
+  const uint32_t blen = (uint32_t)((n - lo) < DF_BLOCK ? (n - lo) : DF_BLOCK);
+  const uint8_t *data = P.base + P.halo + lo;
+  uint32_t *r_blk = P.res + lo;
+  const BlockPrices *bp = reinterpret_cast<const BlockPrices *>(P.slots + (size_t)blk * DF_SLOT);
+  if (bp->any_match == 0) return;  // no match anywhere: the greedy parse is all literals already
+  {
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(bp);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(&s->pr);
+    for (int i = lane; i < (int)(sizeof(BlockPrices) / 4); i += 64) dst[i] = src[i];
+    uint32_t *rw = reinterpret_cast<uint32_t *>(&s->ring[0][0]);
+    for (int i = lane; i < OP_RING * 32; i += 64) rw[i] = 0;
+  }
+  wsync();
+  uint32_t lk[OP_SHORT + 1];  // price << 9 | l of the cut lengths (wave-uniform, SGPRs)
+#pragma unroll
+  for (int l = 3; l <= OP_SHORT; ++l)
+    lk[l] = (uint32_t)__builtin_amdgcn_readfirstlane((int)(((uint32_t)s->pr.lenc[l] << 9) | (uint32_t)l));
+  // backward DP, one segment per lane
+  const uint32_t s0 = (uint32_t)lane * OP_SEG;
+  if (s0 < blen) {
+    const uint32_t seg_end = s0 + OP_SEG < blen ? s0 + OP_SEG : blen;
+    const uint32_t e = seg_end + OP_OV < blen ? seg_end + OP_OV : blen;
+    uint32_t C1 = 0;   // C[i + 1]
+    uint32_t row = 0;  // step mod OP_RING
+    uint32_t cr9[OP_SHORT + 1];  // cr9[l] = C[i + l] << 9 (0 past the segment's end)
+#pragma unroll
+    for (int l = 0; l <= OP_SHORT; ++l) cr9[l] = 0;
+    const uint32_t g_last = (e - 1) & ~15u;
+    const uint32_t ngroups = (g_last - s0) / 16 + 1;
+    const bool d_aligned = (reinterpret_cast<uintptr_t>(data) & 3) == 0;
+    // a group is 16 positions: 64 bytes of res and 16 data bytes per lane, so
+    // the 64 lanes' scattered reads still use whole cache lines
+    auto load_g = [&](uint32_t g, op_u32x4 *r4, op_u32x4 &b4) {
+      const op_u32x4 *src = reinterpret_cast<const op_u32x4 *>(r_blk + g);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) r4[q] = src[q];
+      if (d_aligned && g + 15 < blen) {
+        const uint32_t *d4 = reinterpret_cast<const uint32_t *>(data + g);
+        b4 = op_u32x4{d4[0], d4[1], d4[2], d4[3]};
+      } else {
+        uint32_t w[4] = {0, 0, 0, 0};
+        for (int k = 0; k < 16; ++k)
+          if (g + k < blen) w[k >> 2] |= (uint32_t)data[g + k] << (8 * (k & 3));
+        b4 = op_u32x4{w[0], w[1], w[2], w[3]};
+      }
+    };
+    // OP_PF groups in flight per lane: HBM latency is hidden by depth (one
+    // wave per SIMD here)
+    op_u32x4 rq[OP_PF][4];
+    op_u32x4 bq[OP_PF];
+#pragma unroll
+    for (int j = 0; j < OP_PF; ++j)
+      if ((uint32_t)j < ngroups) load_g(g_last - 16u * (uint32_t)j, rq[j], bq[j]);
+    uint32_t gi = 0;  // groups done
+    while (gi < ngroups) {
+#pragma unroll
+      for (int j = 0; j < OP_PF; ++j) {
+        if (gi < ngroups) {
+          const uint32_t g = g_last - 16u * gi;
+          op_u32x4 rv[4] = {rq[j][0], rq[j][1], rq[j][2], rq[j][3]};
+          const op_u32x4 bv4 = bq[j];
+          if (gi + OP_PF < ngroups) load_g(g - 16u * OP_PF, rq[j], bq[j]);
+#pragma unroll
+          for (int k = 15; k >= 0; --k) {
+            // positions >= e (the tail of the block's last group) are steps
+            // with price 0 and no match: C stays 0 there, as past the end
+            const uint32_t i = g + (uint32_t)k;
+            const bool live = i < e;
+            {
+              const uint32_t r = rv[k >> 2][k & 3];
+              const uint32_t L = live ? r >> 16 : 0u, D = r & 0xFFFF;
+              const uint32_t bv = bv4[k >> 2];
+              // C[i+1 .. i+OP_SHORT] live in registers (cr[1..]); only the
+              // full-length candidate reads the LDS ring.  Candidates are
+              // compared as keys (price relative to C[i+1], biased) << 9 | l.
+              uint32_t eb, ev;
+              const uint32_t Dc = D ? D : 1u;
+              const int dc = (int)s->pr.distc[dist_sym(Dc, eb, ev)];
+              const uint32_t Lc = L < 3 ? 3u : L;
+              const uint32_t rr = row >= Lc ? row - Lc : row + OP_RING - Lc;
+              const int c_far = (int)(int16_t)(uint16_t)(s->ring[rr][lane] - (uint16_t)C1) + (int)s->pr.lenc[Lc];
+              const int lit = live ? (int)s->pr.litc[(bv >> (8 * (k & 3))) & 0xFF] : 0;
+              uint32_t key = (uint32_t)(lit + 0x8000) << 9;
+              // key of length l: (price + C[i+l] - C[i+1] + bias) << 9 | l,
+              // one add3 of pre-shifted terms (exact modulo 2^32: the
+              // unshifted value is below 2^23)
+              const uint32_t base9 = (uint32_t)(dc + 0x8000 - (int)C1) << 9;
+#pragma unroll
+              for (uint32_t l = 3; l < OP_SHORT; l += 2) {
+                const uint32_t ka = base9 + cr9[l] + lk[l], kb = base9 + cr9[l + 1] + lk[l + 1];
+                key = op_min3(key, l <= L ? ka : 0xFFFFFFFFu, l + 1 <= L ? kb : 0xFFFFFFFFu);
+              }
+              {
+                const uint32_t kl = ((uint32_t)(dc + 0x8000 + c_far) << 9) | (Lc & 511);
+                key = (L > OP_SHORT && kl < key) ? kl : key;
+              }
+              const uint32_t choice = key & 511;
+              const int best = (int)(key >> 9) - 0x8000;
+              C1 += (uint32_t)best;
+              s->ring[row][lane] = (uint16_t)C1;
+              row = row + 1 == OP_RING ? 0 : row + 1;
+#pragma unroll
+              for (int l = OP_SHORT; l > 1; --l) cr9[l] = cr9[l - 1];
+              cr9[1] = C1 << 9;
+              rv[k >> 2][k & 3] = choice ? (choice << 16) | D : 0u;
+            }
+          }
+          // the group's choices in whole-line stores (positions >= seg_end
+          // belong to the next lane; a group straddles seg_end only at the
+          // block's end, where the positions past blen are never read)
+          if (g < seg_end) {
+            op_u32x4 *dst = reinterpret_cast<op_u32x4 *>(r_blk + g);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) dst[q] = rv[q];
+          }
+          ++gi;
+        }
+      }
+    }
+  }
 }
 
 __global__ __launch_bounds__(64) void block_kernel(DeflateParams P) {
@@ -782,7 +1089,7 @@ __global__ __launch_bounds__(64) void block_kernel(DeflateParams P) {
   for (int i = lane; i < 288; i += 64) s->lit_hist[i] = 0;
   if (lane < 32) s->dist_hist[lane] = 0;
   wsync();
-  const uint32_t ntok = parse_block(s, P, r_blk, data, blen);
+  const uint32_t ntok = parse_block<true>(s, P, r_blk, data, blen);
   wsync();
   if (lane == 0) s->lit_hist[256] += 1;  // end of block
   wsync();
@@ -1213,14 +1520,15 @@ __global__ __launch_bounds__(256) void stored_blocks(const uint8_t *__restrict__
 
 // ---- host launcher ---------------------------------------------------------------------------
 struct DeflateLevel {
-  int max_chain, nice, lazy, too_far, skip, klen, probe, good;
+  int max_chain, nice, lazy, too_far, skip, klen, probe, good, opt;
 };
 
 static DeflateLevel level_params(int level) {
-  // tuning hook: ZT_DF_PARAMS="max_chain,nice,lazy,skip,klen,probe[,good]" overrides the level
+  // tuning hook: ZT_DF_PARAMS="max_chain,nice,lazy,skip,klen,probe[,good[,opt]]" overrides the level
   if (const char *e = getenv("ZT_DF_PARAMS")) {
-    DeflateLevel L{64, 128, 1, 4096, 128, 8, 16, 8};
-    if (sscanf(e, "%d,%d,%d,%d,%d,%d,%d", &L.max_chain, &L.nice, &L.lazy, &L.skip, &L.klen, &L.probe, &L.good) >= 6)
+    DeflateLevel L{64, 128, 1, 4096, 128, 8, 16, 8, 0};
+    if (sscanf(e, "%d,%d,%d,%d,%d,%d,%d,%d", &L.max_chain, &L.nice, &L.lazy, &L.skip, &L.klen, &L.probe, &L.good,
+               &L.opt) >= 6)
       return L;
   }
   switch (level) {
@@ -1228,15 +1536,15 @@ static DeflateLevel level_params(int level) {
     // 8-byte keys find the long matches (a 3-byte key chain of the same depth
     // sees mostly candidates that cannot win); near probes (registers) find
     // the short ones; a carried match of `good` bytes cuts the chain to 1/4
-    case 1: return {4, 16, 0, 4096, 16, 8, 8, 4};
-    case 2: return {8, 32, 0, 4096, 32, 8, 8, 4};
-    case 3: return {16, 64, 0, 4096, 64, 8, 16, 4};
-    case 4: return {16, 128, 1, 4096, 128, 8, 16, 8};
-    case 5: return {24, 128, 1, 4096, 128, 8, 16, 16};
-    case 7: return {64, 258, 1, 4096, 258, 8, 16, 16};
-    case 8: return {128, 258, 1, 4096, 258, 8, 16, 32};
-    case 9: return {512, 258, 1, 4096, 258, 8, 16, 258};
-    default: return {32, 128, 1, 4096, 128, 8, 16, 16};  // 6
+    case 1: return {4, 16, 0, 4096, 16, 8, 8, 4, 0};
+    case 2: return {8, 32, 0, 4096, 32, 8, 8, 4, 0};
+    case 3: return {16, 64, 0, 4096, 64, 8, 16, 4, 0};
+    case 4: return {16, 128, 1, 4096, 128, 8, 16, 8, 1};
+    case 5: return {24, 128, 1, 4096, 128, 8, 16, 16, 1};
+    case 7: return {64, 258, 1, 4096, 258, 8, 16, 16, 1};
+    case 8: return {128, 258, 1, 4096, 258, 8, 16, 32, 1};
+    case 9: return {512, 258, 1, 4096, 258, 8, 16, 258, 1};
+    default: return {32, 128, 1, 4096, 128, 8, 16, 16, 1};  // 6
   }
 }
 
@@ -1316,6 +1624,7 @@ int deflate_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t halo, in
   P.probe = L.probe;
   P.good = L.good;
   P.ctype = ctype;
+  P.opt = L.opt && ctype == 2;
   P.res = reinterpret_cast<uint32_t *>(sb);
   P.slots = sb + G.res_bytes;
   P.slot_len = reinterpret_cast<uint32_t *>(sb + G.res_bytes + G.slot_bytes);
@@ -1326,6 +1635,12 @@ int deflate_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t halo, in
   match_kernel<<<G.nwg, DF_THREADS, 0, s>>>(P);
   ZT_HIP(hipGetLastError());
   ZT_TRY(timing_end(c, s, 0));
+  if (P.opt) {
+    price_kernel<<<G.nblocks, 64, 0, s>>>(P);
+    ZT_HIP(hipGetLastError());
+    optparse_kernel<<<G.nblocks, 64, 0, s>>>(P);
+    ZT_HIP(hipGetLastError());
+  }
   block_kernel<<<G.nblocks, 64, 0, s>>>(P);
   ZT_HIP(hipGetLastError());
   encode_kernel<<<G.nblocks, ENC_THREADS, 0, s>>>(P);
@@ -1343,6 +1658,15 @@ int deflate_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t halo, in
   *out_len = total;
   return ZT_OK;
 }
+
+#ifdef ZT_DF_TIME
+extern "C" int zt_debug_df_time(unsigned long long *out) {
+  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_df_time), sizeof(unsigned long long) * 4);
+  unsigned long long z[4] = {};
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_df_time), z, sizeof z);
+  return 0;
+}
+#endif
 
 #ifdef ZT_DF_COUNT
 extern "C" int zt_debug_df_count(unsigned long long *out) {
