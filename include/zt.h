@@ -32,6 +32,16 @@ extern "C" {
 #define ZT_E_INVALID_DISTANCE -15        /* RFC 1951 violation the reference does not check (:507) */
 #define ZT_E_INVALID_SYMBOL -16          /* lit/len 286-287 or dist 30-31 used (RFC 1951 3.2.6) */
 #define ZT_E_BAD_TREE -17                /* over-subscribed / empty code-length set */
+/* containers */
+#define ZT_E_GZIP_SIGNATURE -30          /* Error('invalid file signature:ID1,ID2')  src/GUnzip.ts:77 */
+#define ZT_E_GZIP_METHOD -31             /* Error('unknown compression method: CM')  src/GUnzip.ts:82 */
+#define ZT_E_GZIP_HCRC -32               /* Error('invalid header crc16')            src/GUnzip.ts:130 */
+#define ZT_E_GZIP_CRC32 -33              /* Error('invalid CRC-32 checksum: 0x.. / 0x..') src/GUnzip.ts:162 */
+#define ZT_E_GZIP_ISIZE -34              /* Error('invalid input size: N / M')       src/GUnzip.ts:169 */
+#define ZT_E_ZLIB_METHOD -40             /* Error('unsupported compression method')  src/Inflate.ts:47 */
+#define ZT_E_ZLIB_FCHECK -41             /* Error('invalid fcheck flag:N')           src/Inflate.ts:52 */
+#define ZT_E_ZLIB_FDICT -42              /* Error('fdict flag is not supported')     src/Inflate.ts:57 */
+#define ZT_E_ZLIB_ADLER -43              /* Error('invalid adler-32 checksum')       src/Inflate.ts:88 */
 #define ZT_E_NO_DEVICE -100              /* no HIP device: the engine never falls back to the CPU */
 #define ZT_E_HIP -101                    /* HIP runtime failure (see message) */
 #define ZT_E_NOMEM -102
@@ -95,6 +105,55 @@ int zt_inflate_raw_batch(const uint8_t *const *in, const size_t *n, size_t count
                          uint8_t **out, size_t *out_len, size_t *end_ip, int *status);
 int zt_deflate_raw_batch(const uint8_t *const *in, const size_t *n, size_t count, const zt_deflate_opts *opts,
                          uint8_t **out, size_t *out_len, int *status);
+
+/* ---- containers: GZip (RFC 1952) and zlib (RFC 1950) ---------------------- */
+/* The input is uploaded once; the deflate pipeline and the CRC-32 / Adler-32
+ * kernel both read that device copy (the reference deflates, then walks the
+ * input again for the checksum: src/GZip.ts:163-180, src/Deflate.ts:81-85). */
+typedef struct {
+  zt_deflate_opts deflate; /* GZipOptions.deflateOptions */
+  int fname;               /* FNAME: name[0..name_len) is written (GZipOptions.filename) */
+  int fcomment;            /* FCOMMENT: comment[0..comment_len) (GZipOptions.comment) */
+  int fhcrc;               /* FHCRC (GZipOptions.hcrc) */
+  uint32_t mtime;          /* MTIME (the reference writes floor(Date.now()/1000)) */
+  const uint8_t *name;     /* header bytes, already encoded as the reference does */
+  size_t name_len;         /* (charCode <= 0xFF: one byte, else two LE bytes: src/GZip.ts:133-140) */
+  const uint8_t *comment;
+  size_t comment_len;
+} zt_gzip_opts;
+
+/* Replaces new GZip(input, opts).compress()  src/GZip.ts:96-194: one member,
+ * header + raw DEFLATE + CRC-32 + ISIZE.  *crc_out (may be NULL) = GZip.crc32. */
+int zt_gzip_compress(const uint8_t *in, size_t n, const zt_gzip_opts *opts, uint8_t **out, size_t *out_len,
+                     uint32_t *crc_out);
+
+/* One decoded member (GUnzipMember, src/GUnzip.ts:66-175).  Offsets index the
+ * input buffer (name, comment) or the concatenated output (data). */
+typedef struct {
+  uint32_t flg, mtime, xfl, os, xlen;
+  size_t name_off, name_len;       /* valid when flg & FNAME */
+  size_t comment_off, comment_len; /* valid when flg & FCOMMENT */
+  uint32_t has_crc16, crc16;
+  uint32_t crc32, isize;
+  size_t data_off, data_len;
+} zt_gzip_member;
+
+/* Replaces new GUnzip(input).decompress() + getMembers()  src/GUnzip.ts:53-63:
+ * every member until the input is consumed, their outputs concatenated.
+ * *members (free with zt_free; may be NULL) receives *nmembers entries. */
+int zt_gunzip(const uint8_t *in, size_t n, uint8_t **out, size_t *out_len, zt_gzip_member **members,
+              size_t *nmembers);
+
+/* Replaces new Deflate(input, {compressionType, lazy}).compress()
+ * src/Deflate.ts:60-99: CMF/FLG (FLEVEL = compressionType) + raw DEFLATE +
+ * Adler-32 big-endian.  *adler_out (may be NULL) = Deflate.adler32. */
+int zt_zlib_compress(const uint8_t *in, size_t n, const zt_deflate_opts *opts, uint8_t **out, size_t *out_len,
+                     uint32_t *adler_out);
+
+/* Replaces new Inflate(input, {index, verify}).decompress()  src/Inflate.ts:34-93.
+ * *end_ip = Inflate.ip (just past the DEFLATE stream, before the Adler-32). */
+int zt_zlib_decompress(const uint8_t *in, size_t n, size_t index, int verify, uint8_t **out, size_t *out_len,
+                       size_t *end_ip, uint32_t *adler_out);
 
 /* ---- device-resident forms (inputs already in HBM; used by bench.py) ------ */
 /* `stream` is a hipStream_t (NULL = the library's stream for this device).

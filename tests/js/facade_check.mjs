@@ -1,7 +1,7 @@
 // Runs the JS facade (zlib.ts_amd/lib) over cases prepared by
 // tests/test_js_facade.py and prints one JSON result per case.
 import fs from 'fs';
-import { RawDeflate, RawInflate, CRC32, Adler32, deviceCount } from '../../zlib.ts_amd/lib/index.js';
+import { RawDeflate, RawInflate, CRC32, Adler32, GZip, GUnzip, Deflate, Inflate, deviceCount } from '../../zlib.ts_amd/lib/index.js';
 
 const hex = (s) => Uint8Array.from(Buffer.from(s, 'hex'));
 const tohex = (a) => Buffer.from(a.buffer, a.byteOffset, a.length).toString('hex');
@@ -34,6 +34,27 @@ for (const c of cases) {
             const body = s.subarray(opts.outputIndex || 0);
             const back = new RawInflate(body, { refStrict: true }).decompress();
             r.back = tohex(back);
+        } else if (c.op === 'gzip') {
+            const g = new GZip(hex(c.in), c.opts || {});
+            r.out = tohex(g.compress());
+            r.crc32 = g.crc32;
+        } else if (c.op === 'gunzip') {
+            const g = new GUnzip(hex(c.in));
+            r.out = tohex(g.decompress());
+            r.crc32 = g.crc32;
+            r.members = g.getMembers().map((m) => ({
+                flg: m.flg, xfl: m.xfl, os: m.os, mtime: Math.round(m.mtime.getTime() / 1000),
+                name: m.name === undefined ? null : m.name, comment: m.comment === undefined ? null : m.comment,
+                data: tohex(m.data),
+            }));
+        } else if (c.op === 'zlib') {
+            const z = new Deflate(hex(c.in), c.opts || {});
+            r.out = tohex(z.compress());
+            r.adler32 = z.adler32;
+        } else if (c.op === 'zinflate') {
+            const z = new Inflate(hex(c.in), c.opts || {});
+            r.out = tohex(z.decompress());
+            r.ip = z.ip;
         }
     } catch (e) {
         r.error = typeof e === 'string' ? { string: e } : { message: e.message, status: e.ztStatus };

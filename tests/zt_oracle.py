@@ -101,3 +101,101 @@ class Oracle:
         buf = ctypes.create_string_buffer(n or 1)
         self.lib.zo_gen(KINDS[kind], seed, buf, n)
         return buf.raw[:n]
+
+    # ---- containers: host byte logic restated in
+    # Python over the C oracle's RawInflate / CRC32 / Adler32 ----------------
+    @staticmethod
+    def header_bytes(s):
+        """String -> header bytes as src/GZip.ts:133-150 writes them: a char
+        code <= 0xFF is one byte, anything wider two little-endian bytes."""
+        out = bytearray()
+        for ch in s:
+            c = ord(ch)
+            out += bytes([c & 0xFF, (c >> 8) & 0xFF]) if c > 0xFF else bytes([c])
+        return bytes(out)
+
+    def gzip_header(self, name=None, comment=None, hcrc=False, mtime=0):
+        """src/GZip.ts:104-156 (header up to the DEFLATE stream)."""
+        flg = (0x08 if name is not None else 0) | (0x10 if comment is not None else 0) | (0x02 if hcrc else 0)
+        h = bytearray([0x1F, 0x8B, 8, flg]) + mtime.to_bytes(4, "little") + bytes([0, 3])
+        if name is not None:
+            h += name + b"\0"
+        if comment is not None:
+            h += comment + b"\0"
+        if hcrc:
+            h += (self.crc32(bytes(h)) & 0xFFFF).to_bytes(2, "little")
+        return bytes(h)
+
+    def gunzip(self, data):
+        """src/GUnzip.ts:53-175: members until the input is consumed.  Bytes
+        read past the end are `undefined` (0 inside bitwise expressions).
+        Returns (output, members); raises OracleError(msg=reference text)."""
+        n = len(data)
+        u8 = lambda p: data[p] if p < n else 0
+        ip, members = 0, []
+        while ip < n:
+            p = ip
+            if u8(p) != 0x1F or u8(p + 1) != 0x8B:
+                a = str(data[p]) if p < n else "undefined"
+                b = str(data[p + 1]) if p + 1 < n else "undefined"
+                raise OracleError(-30, f"invalid file signature:{a},{b}")
+            if p + 2 >= n or data[p + 2] != 8:
+                raise OracleError(-31, "unknown compression method: " + (str(data[p + 2]) if p + 2 < n else "undefined"))
+            flg = u8(p + 3)
+            m = {"flg": flg, "mtime": int.from_bytes(bytes(u8(p + 4 + k) for k in range(4)), "little"),
+                 "xfl": u8(p + 8), "os": u8(p + 9), "name": None, "comment": None}
+            p += 10
+            if flg & 0x04:
+                p += 2 + (u8(p) | (u8(p + 1) << 8))
+            for bit, key in ((0x08, "name"), (0x10, "comment")):
+                if flg & bit:
+                    e = data.find(b"\0", p)
+                    e = n if e < 0 else e
+                    m[key] = data[p:e]
+                    p = e + 1
+            if flg & 0x02:
+                c16 = self.crc32(data[:p]) & 0xFFFF
+                if c16 != (u8(p) | (u8(p + 1) << 8)):
+                    raise OracleError(-32, "invalid header crc16")
+                p += 2
+            try:
+                out, eip = self.raw_inflate(data, index=p)
+            except OracleError as e:
+                raise OracleError(e.code, e.msg)
+            want = int.from_bytes(bytes(u8(eip + k) for k in range(4)), "little")
+            crc = self.crc32(out)
+            if crc != want:
+                raise OracleError(-33, "invalid CRC-32 checksum: 0x%x / 0x%x" % (crc, want))
+            isize = int.from_bytes(bytes(u8(eip + 4 + k) for k in range(4)), "little")
+            if len(out) & 0xFFFFFFFF != isize:
+                raise OracleError(-34, "invalid input size: %d / %d" % (len(out) & 0xFFFFFFFF, isize))
+            m["data"] = out
+            m["crc32"] = crc
+            members.append(m)
+            ip = eip + 8
+        return b"".join(m["data"] for m in members), members
+
+    def zlib_header(self, compression_type=2):
+        """src/Deflate.ts:67-78: CMF 0x78, FLG with FLEVEL = compressionType."""
+        flg = compression_type << 6
+        return bytes([0x78, flg | (31 - ((0x78 << 8) + flg) % 31)])
+
+    def zlib_inflate(self, data, index=0, verify=False):
+        """src/Inflate.ts:34-93.  Returns (output, ip)."""
+        n = len(data)
+        cmf = data[index] if index < n else None
+        flg = data[index + 1] if index + 1 < n else None
+        if cmf is None or (cmf & 0x0F) != 8:
+            raise OracleError(-40, "unsupported compression method")
+        if flg is None:
+            raise OracleError(-41, "invalid fcheck flag:NaN")
+        if ((cmf << 8) + flg) % 31:
+            raise OracleError(-41, "invalid fcheck flag:%d" % (((cmf << 8) + flg) % 31))
+        if flg & 0x20:
+            raise OracleError(-42, "fdict flag is not supported")
+        out, ip = self.raw_inflate(data, index=index + 2)
+        if verify:
+            want = int.from_bytes(bytes(data[ip + k] if ip + k < n else 0 for k in range(4)), "big")
+            if self.adler32(out) != want:
+                raise OracleError(-43, "invalid adler-32 checksum")
+        return out, ip

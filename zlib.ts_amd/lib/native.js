@@ -24,3 +24,10 @@ export const ZT = {
 export function dflt(v, d) {
     return v === undefined || v === null ? d : v;
 }
+
+// libzt's message is the reference's text; keep the status code beside it
+export function refError(e) {
+    const err = new Error(e.message);
+    if (e.ztStatus !== undefined) err.ztStatus = e.ztStatus;
+    return err;
+}

@@ -163,6 +163,147 @@ napi_value inflate_raw(napi_env env, napi_callback_info info) {
   return obj;
 }
 
+void set_num(napi_env env, napi_value obj, const char *k, double v) {
+  napi_value x;
+  napi_create_double(env, v, &x);
+  napi_set_named_property(env, obj, k, x);
+}
+
+// optional Uint8Array argument (undefined / null -> absent)
+bool opt_u8(napi_env env, napi_value v, const uint8_t **p, size_t *n, bool *present) {
+  napi_valuetype t;
+  napi_typeof(env, v, &t);
+  *present = !(t == napi_undefined || t == napi_null);
+  *p = nullptr;
+  *n = 0;
+  return !*present || get_u8(env, v, p, n);
+}
+
+// gzipCompress(input, compressionType, lazy, level, name|null, comment|null, hcrc, mtime) -> {output, crc32}
+napi_value gzip_compress(napi_env env, napi_callback_info info) {
+  napi_value a[8];
+  args(env, info, a, 8);
+  const uint8_t *p;
+  size_t n;
+  if (!get_u8(env, a[0], &p, &n)) return nullptr;
+  zt_gzip_opts o;
+  memset(&o, 0, sizeof o);
+  o.deflate.compression_type = (int)get_i64(env, a[1], 2);
+  o.deflate.lazy = (int)get_i64(env, a[2], 0);
+  o.deflate.level = (int)get_i64(env, a[3], -1);
+  bool has = false;
+  if (!opt_u8(env, a[4], &o.name, &o.name_len, &has)) return nullptr;
+  o.fname = has;
+  if (!opt_u8(env, a[5], &o.comment, &o.comment_len, &has)) return nullptr;
+  o.fcomment = has;
+  bool hcrc = false;
+  napi_valuetype t;
+  napi_typeof(env, a[6], &t);
+  if (t == napi_boolean) napi_get_value_bool(env, a[6], &hcrc);
+  o.fhcrc = hcrc;
+  o.mtime = get_u32(env, a[7], 0);
+  uint8_t *out = nullptr;
+  size_t olen = 0;
+  uint32_t crc = 0;
+  int rc = zt_gzip_compress(p, n, &o, &out, &olen, &crc);
+  if (rc) return throw_zt(env, rc);
+  napi_value obj;
+  napi_create_object(env, &obj);
+  napi_set_named_property(env, obj, "output", new_u8(env, out, olen));
+  set_num(env, obj, "crc32", crc);
+  return obj;
+}
+
+// gunzip(input) -> {output, members: [{flg, mtime, xfl, os, xlen, nameOff, nameLen, commentOff,
+//                   commentLen, crc16 (or -1), crc32, isize, dataOff, dataLen}]}
+napi_value gunzip(napi_env env, napi_callback_info info) {
+  napi_value a[1];
+  args(env, info, a, 1);
+  const uint8_t *p;
+  size_t n;
+  if (!get_u8(env, a[0], &p, &n)) return nullptr;
+  uint8_t *out = nullptr;
+  size_t olen = 0, cnt = 0;
+  zt_gzip_member *mem = nullptr;
+  int rc = zt_gunzip(p, n, &out, &olen, &mem, &cnt);
+  if (rc) return throw_zt(env, rc);
+  napi_value obj, arr;
+  napi_create_object(env, &obj);
+  napi_set_named_property(env, obj, "output", new_u8(env, out, olen));
+  napi_create_array_with_length(env, cnt, &arr);
+  for (size_t i = 0; i < cnt; ++i) {
+    const zt_gzip_member &m = mem[i];
+    napi_value e;
+    napi_create_object(env, &e);
+    set_num(env, e, "flg", m.flg);
+    set_num(env, e, "mtime", m.mtime);
+    set_num(env, e, "xfl", m.xfl);
+    set_num(env, e, "os", m.os);
+    set_num(env, e, "xlen", m.xlen);
+    set_num(env, e, "nameOff", (double)m.name_off);
+    set_num(env, e, "nameLen", (double)m.name_len);
+    set_num(env, e, "commentOff", (double)m.comment_off);
+    set_num(env, e, "commentLen", (double)m.comment_len);
+    set_num(env, e, "crc16", m.has_crc16 ? (double)m.crc16 : -1.0);
+    set_num(env, e, "crc32", m.crc32);
+    set_num(env, e, "isize", m.isize);
+    set_num(env, e, "dataOff", (double)m.data_off);
+    set_num(env, e, "dataLen", (double)m.data_len);
+    napi_set_element(env, arr, (uint32_t)i, e);
+  }
+  zt_free(mem);
+  napi_set_named_property(env, obj, "members", arr);
+  return obj;
+}
+
+// zlibCompress(input, compressionType, lazy, level) -> {output, adler32}
+napi_value zlib_compress(napi_env env, napi_callback_info info) {
+  napi_value a[4];
+  args(env, info, a, 4);
+  const uint8_t *p;
+  size_t n;
+  if (!get_u8(env, a[0], &p, &n)) return nullptr;
+  zt_deflate_opts o;
+  o.compression_type = (int)get_i64(env, a[1], 2);
+  o.lazy = (int)get_i64(env, a[2], 0);
+  o.level = (int)get_i64(env, a[3], -1);
+  uint8_t *out = nullptr;
+  size_t olen = 0;
+  uint32_t adler = 1;
+  int rc = zt_zlib_compress(p, n, &o, &out, &olen, &adler);
+  if (rc) return throw_zt(env, rc);
+  napi_value obj;
+  napi_create_object(env, &obj);
+  napi_set_named_property(env, obj, "output", new_u8(env, out, olen));
+  set_num(env, obj, "adler32", adler);
+  return obj;
+}
+
+// zlibDecompress(input, index, verify) -> {output, ip, adler32}
+napi_value zlib_decompress(napi_env env, napi_callback_info info) {
+  napi_value a[3];
+  args(env, info, a, 3);
+  const uint8_t *p;
+  size_t n;
+  if (!get_u8(env, a[0], &p, &n)) return nullptr;
+  const int64_t index = get_i64(env, a[1], 0);
+  bool verify = false;
+  napi_valuetype t;
+  napi_typeof(env, a[2], &t);
+  if (t == napi_boolean) napi_get_value_bool(env, a[2], &verify);
+  uint8_t *out = nullptr;
+  size_t olen = 0, ip = 0;
+  uint32_t adler = 1;
+  int rc = zt_zlib_decompress(p, n, index < 0 ? 0 : (size_t)index, verify, &out, &olen, &ip, &adler);
+  if (rc) return throw_zt(env, rc);
+  napi_value obj;
+  napi_create_object(env, &obj);
+  napi_set_named_property(env, obj, "output", new_u8(env, out, olen));
+  set_num(env, obj, "ip", (double)ip);
+  set_num(env, obj, "adler32", adler);
+  return obj;
+}
+
 napi_value device_count(napi_env env, napi_callback_info) {
   napi_value r;
   napi_create_int32(env, zt_device_count(), &r);
@@ -181,6 +322,10 @@ napi_value init(napi_env env, napi_value exports) {
       {"adler32Update", nullptr, adler32_update, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"deflateRaw", nullptr, deflate_raw, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"inflateRaw", nullptr, inflate_raw, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+      {"gzipCompress", nullptr, gzip_compress, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+      {"gunzip", nullptr, gunzip, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+      {"zlibCompress", nullptr, zlib_compress, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+      {"zlibDecompress", nullptr, zlib_decompress, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"deviceCount", nullptr, device_count, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"version", nullptr, version, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
   };

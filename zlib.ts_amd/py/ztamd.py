@@ -14,7 +14,10 @@ ZT_OK = 0
 ERRORS = {
     -1: "ZT_E_INVALID_COMPRESSION_TYPE", -2: "ZT_E_INVALID_INDEX", -10: "ZT_E_INPUT_BROKEN",
     -11: "ZT_E_INVALID_CODE_LENGTH", -12: "ZT_E_UNKNOWN_BTYPE", -13: "ZT_E_STORED_LEN", -14: "ZT_E_STORED_NLEN",
-    -15: "ZT_E_INVALID_DISTANCE", -16: "ZT_E_INVALID_SYMBOL", -17: "ZT_E_BAD_TREE", -100: "ZT_E_NO_DEVICE",
+    -15: "ZT_E_INVALID_DISTANCE", -16: "ZT_E_INVALID_SYMBOL", -17: "ZT_E_BAD_TREE",
+    -30: "ZT_E_GZIP_SIGNATURE", -31: "ZT_E_GZIP_METHOD", -32: "ZT_E_GZIP_HCRC", -33: "ZT_E_GZIP_CRC32",
+    -34: "ZT_E_GZIP_ISIZE", -40: "ZT_E_ZLIB_METHOD", -41: "ZT_E_ZLIB_FCHECK", -42: "ZT_E_ZLIB_FDICT",
+    -43: "ZT_E_ZLIB_ADLER", -100: "ZT_E_NO_DEVICE",
     -101: "ZT_E_HIP", -102: "ZT_E_NOMEM", -103: "ZT_E_ARG",
 }
 
@@ -39,6 +42,20 @@ class KernelTimes(ctypes.Structure):
 
 class InflateOpts(ctypes.Structure):
     _fields_ = [("buffer_type", ctypes.c_int), ("buffer_size", ctypes.c_size_t), ("ref_strict", ctypes.c_int)]
+
+
+class GzipOpts(ctypes.Structure):
+    _fields_ = [("deflate", DeflateOpts), ("fname", ctypes.c_int), ("fcomment", ctypes.c_int),
+                ("fhcrc", ctypes.c_int), ("mtime", ctypes.c_uint32), ("name", ctypes.c_char_p),
+                ("name_len", ctypes.c_size_t), ("comment", ctypes.c_char_p), ("comment_len", ctypes.c_size_t)]
+
+
+class GzipMember(ctypes.Structure):
+    _fields_ = [("flg", ctypes.c_uint32), ("mtime", ctypes.c_uint32), ("xfl", ctypes.c_uint32),
+                ("os", ctypes.c_uint32), ("xlen", ctypes.c_uint32), ("name_off", ctypes.c_size_t),
+                ("name_len", ctypes.c_size_t), ("comment_off", ctypes.c_size_t), ("comment_len", ctypes.c_size_t),
+                ("has_crc16", ctypes.c_uint32), ("crc16", ctypes.c_uint32), ("crc32", ctypes.c_uint32),
+                ("isize", ctypes.c_uint32), ("data_off", ctypes.c_size_t), ("data_len", ctypes.c_size_t)]
 
 
 def _load():
@@ -69,6 +86,10 @@ def _load():
         "zt_inflate_raw_batch": ([P(vp), P(sz), sz, P(InflateOpts), u8pp, P(sz), P(sz), P(ctypes.c_int)],
                                  ctypes.c_int),
         "zt_deflate_raw_batch": ([P(vp), P(sz), sz, P(DeflateOpts), u8pp, P(sz), P(ctypes.c_int)], ctypes.c_int),
+        "zt_gzip_compress": ([vp, sz, P(GzipOpts), u8pp, P(sz), P(u32)], ctypes.c_int),
+        "zt_gunzip": ([vp, sz, u8pp, P(sz), P(P(GzipMember)), P(sz)], ctypes.c_int),
+        "zt_zlib_compress": ([vp, sz, P(DeflateOpts), u8pp, P(sz), P(u32)], ctypes.c_int),
+        "zt_zlib_decompress": ([vp, sz, sz, ctypes.c_int, u8pp, P(sz), P(sz), P(u32)], ctypes.c_int),
         "zt_dev_checksums": ([vp, sz, u32, u32, P(u32), P(u32), vp], ctypes.c_int),
         "zt_deflate_plan_create": ([sz, P(DeflateOpts), P(vp)], ctypes.c_int),
         "zt_deflate_plan_destroy": ([vp], None),
@@ -96,7 +117,8 @@ lib = _load()
 SYMBOLS = [
     "zt_device_count", "zt_set_device", "zt_last_error_message", "zt_version", "zt_free", "zt_crc32_update",
     "zt_adler32_update", "zt_checksums", "zt_deflate_raw", "zt_inflate_raw", "zt_inflate_raw_batch",
-    "zt_deflate_raw_batch", "zt_dev_checksums", "zt_deflate_plan_create", "zt_deflate_plan_destroy",
+    "zt_deflate_raw_batch", "zt_gzip_compress", "zt_gunzip", "zt_zlib_compress", "zt_zlib_decompress",
+    "zt_dev_checksums", "zt_deflate_plan_create", "zt_deflate_plan_destroy",
     "zt_deflate_bound", "zt_deflate_dev", "zt_inflate_plan_create", "zt_inflate_plan_destroy", "zt_inflate_dev",
     "zt_synth_dev", "zt_timing_enable", "zt_timing_read",
 ]
@@ -205,6 +227,76 @@ def deflate_raw_batch(items, compression_type=2, level=-1):
         res.append(ctypes.string_at(outs[i], olens[i]))
         lib.zt_free(outs[i])
     return res
+
+
+def _take(out, olen):
+    res = ctypes.string_at(out, olen.value)
+    lib.zt_free(out)
+    return res
+
+
+def gzip_compress(data, name=None, comment=None, hcrc=False, mtime=0, compression_type=2, lazy=0, level=-1):
+    """GZip.compress (src/GZip.ts:96-194); name/comment are header bytes.
+    Returns (member bytes, crc32)."""
+    b, n = _cbuf(data)
+    o = GzipOpts()
+    o.deflate = DeflateOpts(compression_type, lazy, level)
+    o.fname, o.fcomment, o.fhcrc, o.mtime = int(name is not None), int(comment is not None), int(hcrc), mtime
+    if name is not None:
+        o.name, o.name_len = bytes(name), len(name)
+    if comment is not None:
+        o.comment, o.comment_len = bytes(comment), len(comment)
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    olen = ctypes.c_size_t()
+    crc = ctypes.c_uint32()
+    _check(lib.zt_gzip_compress(b, n, ctypes.byref(o), ctypes.byref(out), ctypes.byref(olen), ctypes.byref(crc)))
+    return _take(out, olen), crc.value
+
+
+def gunzip(data):
+    """GUnzip.decompress + getMembers (src/GUnzip.ts:43-175).  Returns
+    (output, [member dicts])."""
+    b, n = _cbuf(data)
+    raw = bytes(data)
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    olen = ctypes.c_size_t()
+    mem = ctypes.POINTER(GzipMember)()
+    cnt = ctypes.c_size_t()
+    _check(lib.zt_gunzip(b, n, ctypes.byref(out), ctypes.byref(olen), ctypes.byref(mem), ctypes.byref(cnt)))
+    res = _take(out, olen)
+    members = []
+    for i in range(cnt.value):
+        m = mem[i]
+        d = {k: getattr(m, k) for k, _ in GzipMember._fields_}
+        d["name"] = raw[m.name_off:m.name_off + m.name_len] if m.flg & 0x08 else None
+        d["comment"] = raw[m.comment_off:m.comment_off + m.comment_len] if m.flg & 0x10 else None
+        d["data"] = res[m.data_off:m.data_off + m.data_len]
+        members.append(d)
+    lib.zt_free(mem)
+    return res, members
+
+
+def zlib_compress(data, compression_type=2, lazy=0, level=-1):
+    """Deflate.compress (src/Deflate.ts:60-99).  Returns (stream, adler32)."""
+    b, n = _cbuf(data)
+    o = DeflateOpts(compression_type, lazy, level)
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    olen = ctypes.c_size_t()
+    adler = ctypes.c_uint32()
+    _check(lib.zt_zlib_compress(b, n, ctypes.byref(o), ctypes.byref(out), ctypes.byref(olen), ctypes.byref(adler)))
+    return _take(out, olen), adler.value
+
+
+def zlib_decompress(data, index=0, verify=False):
+    """Inflate.decompress (src/Inflate.ts:34-93).  Returns (output, ip)."""
+    b, n = _cbuf(data)
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    olen = ctypes.c_size_t()
+    ip = ctypes.c_size_t()
+    adler = ctypes.c_uint32()
+    _check(lib.zt_zlib_decompress(b, n, index, int(verify), ctypes.byref(out), ctypes.byref(olen), ctypes.byref(ip),
+                                  ctypes.byref(adler)))
+    return _take(out, olen), ip.value
 
 
 # ---- device-resident helpers (torch tensors as HBM buffers) -----------------------
