@@ -143,6 +143,12 @@ struct MatchShared {
   uint32_t work;                    // next super-step of 256 positions to search
 };
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS
+// operations, not for its global loads (the next sub-chunk's prefetch stays
+// in flight) nor its global stores (res[] is read by later kernels only).
+// __syncthreads() would drain vmcnt and expose HBM latency at every barrier.
+__device__ __forceinline__ void lds_barrier() { __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 __device__ __forceinline__ uint32_t ridx(uint32_t rel) { return rel & (DF_RING - 1); }
 __device__ __forceinline__ uint32_t ld8(const MatchShared *s, uint32_t rel) {
   return reinterpret_cast<const uint8_t *>(s->ring)[ridx(rel)];
@@ -287,6 +293,21 @@ __device__ __forceinline__ void near_probe(const uint32_t (&w)[8], uint32_t cur0
   }
 }
 
+// Branch-free prefilter of the near probes of position pb + K: the minimum
+// over distances 1..DF_NEAR of (3 bytes at p - D) XOR (3 bytes at p) is zero
+// iff some distance has a 3-byte match (out-of-range distances only give
+// false positives; near_probe re-checks).  One alignbyte + bitop3 + min per
+// distance instead of a compare-and-branch per distance.
+template <int K, int D>
+__device__ __forceinline__ uint32_t near_any(const uint32_t (&w)[8], uint32_t cur0, uint32_t m) {
+  if constexpr (D <= DF_NEAR) {
+    const uint32_t x = (win32<16 + K - D>(w) ^ cur0) & 0xFFFFFFu;
+    return near_any<K, D + 1>(w, cur0, m < x ? m : x);
+  } else {
+    return m;
+  }
+}
+
 // One position's hash-chain walk (newest candidate first).  Two walks are
 // interleaved per thread so that their dependent LDS loads overlap.
 struct Walk {
@@ -399,9 +420,9 @@ __device__ __forceinline__ void walk_pair_step(Walk &a, Walk &b, const MatchShar
 // finish position pb + K: near probes when the chain found nothing long
 template <int K>
 __device__ __forceinline__ uint32_t walk_finish(const Walk &w, const DeflateParams &P, const uint32_t (&win)[8],
-                                                uint32_t &carry_len, uint32_t &carry_dist) {
+                                                uint32_t near, uint32_t &carry_len, uint32_t &carry_dist) {
   uint32_t best_len = w.best_len, best_dist = w.best_dist;
-  if (w.max_len >= 3 && best_len < (uint32_t)P.klen)
+  if (near == 0 && w.max_len >= 3 && best_len < (uint32_t)P.klen)
     near_probe<K, 1>(win, w.cur, w.cur2, w.p, w.max_len, P.probe, best_len, best_dist);
   carry_len = best_len;
   carry_dist = best_dist;
@@ -421,17 +442,19 @@ __device__ void search_quad(const MatchShared *s, const DeflateParams &P, uint32
   // positions 0 and 2 walk together, then 1 and 3 with the carry of 0 and 2
   uint32_t out[4];
   uint32_t c0l, c0d, c2l, c2d, cl, cd;
+  const uint32_t nr0 = near_any<0, 1>(w, win32<16>(w), ~0u), nr1 = near_any<1, 1>(w, win32<17>(w), ~0u);
+  const uint32_t nr2 = near_any<2, 1>(w, win32<18>(w), ~0u), nr3 = near_any<3, 1>(w, win32<19>(w), ~0u);
   Walk wa, wb;
   walk_init(wa, s, P, pb, p1, win32<16>(w), win32<20>(w), 0, 0);
   walk_init(wb, s, P, pb + 2, p1, win32<18>(w), win32<22>(w), 0, 0);
   while (wa.active || wb.active) walk_pair_step(wa, wb, s, P, key);
-  out[0] = walk_finish<0>(wa, P, w, c0l, c0d);
-  out[2] = walk_finish<2>(wb, P, w, c2l, c2d);
+  out[0] = walk_finish<0>(wa, P, w, nr0, c0l, c0d);
+  out[2] = walk_finish<2>(wb, P, w, nr2, c2l, c2d);
   walk_init(wa, s, P, pb + 1, p1, win32<17>(w), win32<21>(w), c0l, c0d);
   walk_init(wb, s, P, pb + 3, p1, win32<19>(w), win32<23>(w), c2l, c2d);
   while (wa.active || wb.active) walk_pair_step(wa, wb, s, P, key);
-  out[1] = walk_finish<1>(wa, P, w, cl, cd);
-  out[3] = walk_finish<3>(wb, P, w, cl, cd);
+  out[1] = walk_finish<1>(wa, P, w, nr1, cl, cd);
+  out[3] = walk_finish<3>(wb, P, w, nr3, cl, cd);
   if (pb + 4 <= p1) {
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     u32x4 v = {out[0], out[1], out[2], out[3]};
@@ -470,7 +493,7 @@ __global__ __launch_bounds__(DF_THREADS) void match_kernel(DeflateParams P) {
   const bool g_aligned = (reinterpret_cast<uintptr_t>(g) & 3) == 0;
   for (uint32_t p0 = 0; p0 < re; p0 += DF_SUB) {
     const uint32_t p1 = (p0 + DF_SUB) < re ? (p0 + DF_SUB) : re;
-    __syncthreads();
+    lds_barrier();
     uint64_t t0, t1, t2, t3;
     DF_T(t0);
     uint32_t ih = p1 >= kext ? p1 - kext : 0;
@@ -486,7 +509,7 @@ __global__ __launch_bounds__(DF_THREADS) void match_kernel(DeflateParams P) {
     const bool fast = g_aligned && n0 + DF_SUB <= re;
     uint32_t nv = 0;
     if (fast) nv = reinterpret_cast<const uint32_t *>(g + n0)[t];
-    __syncthreads();
+    lds_barrier();
     DF_T(t1);
     // wave 0 links the chains step by step; every wave (wave 0 once done)
     // takes super-steps of 256 positions in order and searches them as soon
@@ -508,7 +531,7 @@ __global__ __launch_bounds__(DF_THREADS) void match_kernel(DeflateParams P) {
       }
     }
     DF_T(t2);
-    __syncthreads();
+    lds_barrier();
     DF_T(t3);
 #ifdef ZT_DF_TIME
     if (t == 0) {
