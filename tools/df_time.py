@@ -2,7 +2,7 @@
 # chain build (of which serial linking), search, wait at the barrier after search.
 import ctypes, os, sys; sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', 'zlib.ts_amd', 'py'))
 import torch, ztamd as zt
-buf = (ctypes.c_ulonglong * 4)()
+buf = (ctypes.c_ulonglong * 8)()
 for kind in sys.argv[1:]:
     n = 128 << 20
     d_in = torch.empty(n, dtype=torch.uint8, device="cuda")
@@ -15,5 +15,5 @@ for kind in sys.argv[1:]:
     zt.lib.zt_debug_df_time(buf)
     v = list(buf)
     subs = v[3] & ((1 << 20) - 1)
-    link = v[3] >> 20
+    link = v[4]
     print(f"{kind:10s} sub-chunks {subs}  cycles/sub: chain_build {v[0]/subs:8.0f} (link {link/subs:8.0f})  search(t0) {v[1]/subs:8.0f}  barrier wait {v[2]/subs:8.0f}", flush=True)

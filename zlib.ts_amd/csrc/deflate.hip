@@ -39,7 +39,7 @@
 namespace zt {
 
 #ifdef ZT_DF_TIME
-__device__ unsigned long long g_df_time[4];  // debug: cycles (thread 0 of each workgroup) in phases
+__device__ unsigned long long g_df_time[8];  // debug: cycles (thread 0 of each workgroup) in phases
 #define DF_T(v) v = __builtin_readcyclecounter()
 #else
 #define DF_T(v) (void)0
@@ -52,10 +52,9 @@ constexpr int DF_BLOCK = 32768;
 constexpr int DF_SUB = 4096;
 constexpr int DF_RING = 32768;  // power of two: ring index = rel & (DF_RING - 1)
 constexpr int DF_SLOT = DF_BLOCK + DF_BLOCK / 8 + 1024;  // per-block slot: fits a forced fixed-code block
-#ifndef ZT_DF_HBITS
-#define ZT_DF_HBITS 14
-#endif
-constexpr int DF_HBITS = ZT_DF_HBITS;
+// hash buckets: 2^14 minus 32 (the u32 head table leaves room in the 160 KiB
+// of LDS for the ring's wrap mirror and the work counters)
+constexpr uint32_t DF_HSIZE = (1u << 14) - 32;
 constexpr int DF_THREADS = 1024;
 // the ring holds [p1 - DF_RING, p1) while sub-chunk [p0, p1) is searched;
 // a super-chunk loads DF_HIST bytes of history first (whole sub-chunks)
@@ -64,8 +63,8 @@ constexpr int DF_MAXDIST = DF_HIST - 64;      // 28608
 constexpr int ENC_THREADS = 256;
 // Independent segments of 1 MiB: restart points for segment-parallel inflate
 constexpr uint32_t kRestartBlocks = 32;
-// empty head entry: p - kNoHead (mod 2^16) exceeds DF_MAXDIST for p < 25536
-constexpr uint16_t kNoHead = (uint16_t)(65536 - 40000);
+// empty head entry: p - kNoHead exceeds DF_MAXDIST for every rel position p
+constexpr uint32_t kNoHead = 0x80000000u;
 
 struct BlockPlan;
 
@@ -137,8 +136,8 @@ __device__ __forceinline__ uint32_t len_sym(uint32_t L) {  // 0..28 (symbol - 25
 struct MatchShared {
   uint32_t ring[DF_RING / 4 + 16];  // data ring + 64-byte mirror of its start
   uint16_t prev[DF_RING];           // relative chain links (0 = none)
-  uint16_t head[1 << DF_HBITS];     // newest position (rel) per hash, mod 2^16 (see chain_build)
-  uint16_t hbuf[DF_SUB + 64];       // hashes of the positions being linked
+  uint32_t head[DF_HSIZE];          // newest position (rel) per hash bucket
+  uint32_t dummy[2];                // exchange / link target of lanes past the end (branch-free chain_link)
   uint32_t linked;                  // positions below are linked (chain_link -> searching waves)
   uint32_t work;                    // next super-step of 256 positions to search
 };
@@ -163,9 +162,9 @@ struct Key {
   uint32_t kmask, kmask2;
 };
 __device__ __forceinline__ uint32_t key_hash(const MatchShared *s, uint32_t p, Key k) {
-  uint32_t v = ld32(s, p) & k.kmask;
-  if (k.kmask2) v ^= (ld32(s, p + 4) & k.kmask2) * 0x2545F491u;
-  return (v * 0x9E3779B1u) >> (32 - DF_HBITS);
+  // branch-free (a uniform branch here makes the compiler wait for each load)
+  const uint32_t v = (ld32(s, p) & k.kmask) ^ ((ld32(s, p + 4) & k.kmask2) * 0x2545F491u);
+  return __umulhi(v * 0x9E3779B1u, DF_HSIZE);
 }
 
 // bytes [rel0, rel0 + len) of the super-chunk into the ring (len <= DF_SUB, rel0 % DF_SUB == 0)
@@ -187,72 +186,46 @@ __device__ void load_sub(MatchShared *s, const uint8_t *g, uint32_t rel0, uint32
   }
 }
 
-// chain links for positions [lo, hi) (rel coords, hi - lo <= DF_SUB + 3), in two parts:
-// chain_hash (all waves): hashes, and each position's predecessor inside its
-//   step of 64 by ballot peer masks (bit 15 of prev: last of its hash in the step)
-// chain_link (one wave): links the step leaders to the head table in position
-//   order, publishing its progress in s->linked while the other waves search
-//   the positions already linked (match_kernel)
-__device__ void chain_hash(MatchShared *s, uint32_t lo, uint32_t hi, Key key) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t nsteps = (hi - lo + 63) / 64;
-  for (uint32_t st = wave; st < nsteps; st += DF_THREADS / 64) {
-    const uint32_t p = lo + st * 64 + lane;
-    const bool valid = p < hi;
-    const uint32_t h = valid ? key_hash(s, p, key) : 0;
-    uint64_t peers = __ballot(valid);
-#pragma unroll
-    for (int b = 0; b < DF_HBITS; ++b) {
-      uint64_t m = __ballot((h >> b) & 1);
-      peers &= ((h >> b) & 1) ? m : ~m;
-    }
-    const uint64_t below = peers & lanemask_lt(lane);
-    const uint64_t above = peers & ~((2ull << lane) - 1);
-    const uint32_t d = below ? (uint32_t)(lane - (63 - __clzll(below))) : 0u;
-    if (valid) {
-      s->prev[ridx(p)] = (uint16_t)(d | (above ? 0 : 0x8000));
-      s->hbuf[p - lo] = (uint16_t)h;
-    }
-  }
-}
-
-constexpr int CB_PF = 4;  // steps whose (prev, hash) pairs are read ahead; progress published per CB_PF steps
-__device__ void chain_link(MatchShared *s, uint32_t lo, uint32_t hi) {
+// chain links for positions [lo, hi) (rel coords), by one wave, in position
+// order: per step of 64 positions one LDS exchange head[h] <-> p.  The LDS
+// applies the conflicting lanes of one exchange in lane order (checked on
+// gfx950 by tools/micro/lds_xchg_order.hip), so each lane gets the newest
+// earlier position of its bucket -- in its step or before -- and the head
+// ends at the step's last one.  Exchanges of later steps are issued without
+// waiting for earlier results (the wave's LDS operations stay in order); the
+// progress is published in s->linked for the searching waves (match_kernel).
+constexpr int CL_U = 8;  // steps per group: hashes, then exchanges, then links
+__device__ void chain_link(MatchShared *s, uint32_t lo, uint32_t hi, Key key) {
   const int lane = threadIdx.x & 63;
   const uint32_t nsteps = (hi - lo + 63) / 64;
-  uint32_t eh[CB_PF];  // prev | hash << 16 of step st + j
-  // branch-free reads: a branch join would make the compiler wait for every
-  // LDS load in flight
-  auto fetch = [&](uint32_t st) -> uint32_t {
-    const uint32_t p = lo + st * 64 + lane;
-    const uint32_t pc = p < hi ? p : lo;
-    const uint32_t v = (uint32_t)s->prev[ridx(pc)] | ((uint32_t)s->hbuf[pc - lo] << 16);
-    return p < hi ? v : 1u;
-  };
+  uint32_t hq[CL_U];
+  auto hashes = [&](uint32_t sb, uint32_t (&h)[CL_U]) {
 #pragma unroll
-  for (int j = 0; j < CB_PF; ++j) eh[j] = fetch(j);
-  for (uint32_t sb = 0; sb < nsteps; sb += CB_PF) {
-#pragma unroll
-    for (int j = 0; j < CB_PF; ++j) {
-      const uint32_t st = sb + j;
-      if (st < nsteps) {
-        const uint32_t p = lo + st * 64 + lane;
-        const uint32_t e = eh[j] & 0xFFFF, h = eh[j] >> 16;
-        // the head read is issued before the read-ahead, so waiting for it
-        // leaves the read-ahead in flight
-        const uint32_t hd = s->head[h];
-        eh[j] = fetch(st + CB_PF);
-        // heads are kept mod 2^16: an entry 2^16 or more positions old
-        // aliases a recent position of another hash, which only costs a
-        // hop (every candidate is verified byte by byte); d <= p keeps
-        // the link inside the loaded range
-        const uint32_t d = (uint16_t)(p - hd);
-        const uint32_t link = (e & 0x7F) ? (e & 0x7F) : (d <= DF_MAXDIST && d <= p ? d : 0u);
-        if (p < hi) s->prev[ridx(p)] = (uint16_t)link;
-        if (p < hi && (e & 0x8000)) s->head[h] = (uint16_t)p;
-      }
+    for (int j = 0; j < CL_U; ++j) {
+      const uint32_t p = lo + (sb + j) * 64 + lane;
+      h[j] = key_hash(s, p < hi ? p : lo, key);
     }
-    const uint32_t done = lo + (sb + CB_PF) * 64;
+  };
+  hashes(0, hq);
+  for (uint32_t sb = 0; sb < nsteps; sb += CL_U) {
+    // branch-free: lanes past hi exchange with / link into a dummy word, so
+    // the compiler keeps every load and exchange of the group in flight
+    uint32_t old[CL_U];
+#pragma unroll
+    for (int j = 0; j < CL_U; ++j) {
+      const uint32_t p = lo + (sb + j) * 64 + lane;
+      uint32_t *hp = p < hi ? &s->head[hq[j]] : &s->dummy[0];
+      old[j] = atomicExch(hp, p);
+    }
+    hashes(sb + CL_U, hq);
+#pragma unroll
+    for (int j = 0; j < CL_U; ++j) {
+      const uint32_t p = lo + (sb + j) * 64 + lane;
+      const uint32_t d = p - old[j];
+      uint16_t *pp = p < hi ? &s->prev[ridx(p)] : reinterpret_cast<uint16_t *>(&s->dummy[1]);
+      *pp = (uint16_t)(d <= (uint32_t)DF_MAXDIST ? d : 0u);
+    }
+    const uint32_t done = lo + (sb + CL_U) * 64;
     if (lane == 0)
       __hip_atomic_store(&s->linked, done < hi ? done : hi, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
@@ -486,7 +459,7 @@ __global__ __launch_bounds__(DF_THREADS) void match_kernel(DeflateParams P) {
   key.kmask2 = P.klen >= 8 ? 0xFFFFFFFFu : P.klen == 6 ? 0xFFFFu : P.klen == 5 ? 0xFFu : 0u;
   const uint32_t kext = (uint32_t)P.klen - 1;  // a key at p needs bytes up to p + kext
 
-  for (uint32_t i = t; i < (1u << DF_HBITS); i += DF_THREADS) s.head[i] = kNoHead;
+  for (uint32_t i = t; i < DF_HSIZE; i += DF_THREADS) s.head[i] = kNoHead;
   __syncthreads();
   uint32_t inserted = 0;  // positions [0, inserted) are in the chains
   if (re > 0) load_sub(&s, g, 0, re < DF_SUB ? re : DF_SUB);
@@ -499,7 +472,6 @@ __global__ __launch_bounds__(DF_THREADS) void match_kernel(DeflateParams P) {
     uint32_t ih = p1 >= kext ? p1 - kext : 0;
     if (rend >= kext && ih > rend - kext) ih = rend - kext;
     const bool link = ih > inserted;
-    if (link) chain_hash(&s, inserted, ih, key);
     if (t == 0) {
       s.linked = link ? inserted : ih;
       s.work = 0;
@@ -514,7 +486,12 @@ __global__ __launch_bounds__(DF_THREADS) void match_kernel(DeflateParams P) {
     // wave 0 links the chains step by step; every wave (wave 0 once done)
     // takes super-steps of 256 positions in order and searches them as soon
     // as their links are final (positions only read links of older ones)
-    if (t < 64 && link) chain_link(&s, inserted, ih);
+    if (t < 64 && link) chain_link(&s, inserted, ih, key);
+#ifdef ZT_DF_TIME
+    uint64_t tl;
+    DF_T(tl);
+    if (t == 0) atomicAdd(&g_df_time[4], (unsigned long long)(tl - t1));
+#endif
     inserted = link ? ih : inserted;
     if (p0 >= rs) {
       const uint32_t nss = (p1 - p0 + 255) / 256;
@@ -1684,8 +1661,8 @@ int deflate_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t halo, in
 
 #ifdef ZT_DF_TIME
 extern "C" int zt_debug_df_time(unsigned long long *out) {
-  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_df_time), sizeof(unsigned long long) * 4);
-  unsigned long long z[4] = {};
+  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_df_time), sizeof(unsigned long long) * 8);
+  unsigned long long z[8] = {};
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_df_time), z, sizeof z);
   return 0;
 }
