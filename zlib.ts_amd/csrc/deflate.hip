@@ -233,7 +233,7 @@ __device__ void chain_link(MatchShared *s, uint32_t lo, uint32_t hi, Key key) {
 
 // 4 bytes at byte x of a register window (x a compile-time constant after unrolling)
 template <int X>
-__device__ __forceinline__ uint32_t win32(const uint32_t (&w)[8]) {
+__device__ __forceinline__ uint32_t win32(const uint32_t (&w)[9]) {
   return (X & 3) ? __builtin_amdgcn_alignbyte(w[(X >> 2) + 1], w[X >> 2], X & 3) : w[X >> 2];
 }
 
@@ -242,7 +242,7 @@ constexpr int DF_NEAR = 16;  // near distances probed from registers
 // matches shorter than the chain key at distances 1..probe, from a register
 // window of bytes [pb - 16, pb + 16): longest wins, ties to the nearest
 template <int K, int D>
-__device__ __forceinline__ void near_probe(const uint32_t (&w)[8], uint32_t cur0, uint32_t cur1, uint32_t p,
+__device__ __forceinline__ void near_probe(const uint32_t (&w)[9], uint32_t cur0, uint32_t cur1, uint32_t p,
                                            uint32_t max_len, int probe, uint32_t &best_len, uint32_t &best_dist) {
   if constexpr (D <= DF_NEAR) {
     if (D <= probe && (uint32_t)D <= p) {
@@ -272,7 +272,7 @@ __device__ __forceinline__ void near_probe(const uint32_t (&w)[8], uint32_t cur0
 // false positives; near_probe re-checks).  One alignbyte + bitop3 + min per
 // distance instead of a compare-and-branch per distance.
 template <int K, int D>
-__device__ __forceinline__ uint32_t near_any(const uint32_t (&w)[8], uint32_t cur0, uint32_t m) {
+__device__ __forceinline__ uint32_t near_any(const uint32_t (&w)[9], uint32_t cur0, uint32_t m) {
   if constexpr (D <= DF_NEAR) {
     const uint32_t x = (win32<16 + K - D>(w) ^ cur0) & 0xFFFFFFu;
     return near_any<K, D + 1>(w, cur0, m < x ? m : x);
@@ -284,18 +284,34 @@ __device__ __forceinline__ uint32_t near_any(const uint32_t (&w)[8], uint32_t cu
 // One position's hash-chain walk (newest candidate first).  Two walks are
 // interleaved per thread so that their dependent LDS loads overlap.
 struct Walk {
-  uint32_t p, q, link, max_len, best_len, best_dist, o, pw, cur, cur2;
+  uint32_t p, q, link, max_len, best_len, best_dist, o, pw, omask, cur, cur2, cur3, cur4;
   int hops, max_hops;
   bool active;
 };
 
-// start the walk of position p (carry: the previous position's match)
+// n words at byte rel of the ring, unaligned (the 64-byte mirror past the
+// ring's end keeps up to 15 words contiguous): n + 1 dword loads, no wrap math
+template <int N>
+__device__ __forceinline__ void ld_run(const MatchShared *s, uint32_t rel, uint32_t (&o)[N]) {
+  const uint32_t i = ridx(rel), w = i >> 2, sh = i & 3;
+  uint32_t d[N + 1];
+#pragma unroll
+  for (int k = 0; k <= N; ++k) d[k] = s->ring[w + k];
+#pragma unroll
+  for (int k = 0; k < N; ++k) o[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+}
+
+// start the walk of position p (carry: the previous position's match); cur..cur4
+// are bytes 0..15 of p
 __device__ __forceinline__ void walk_init(Walk &w, const MatchShared *s, const DeflateParams &P, uint32_t p, uint32_t p1,
-                                          uint32_t cur, uint32_t cur2, uint32_t carry_len, uint32_t carry_dist) {
+                                          uint32_t cur, uint32_t cur2, uint32_t cur3, uint32_t cur4,
+                                          uint32_t carry_len, uint32_t carry_dist) {
   w.p = p;
   w.q = p;
   w.cur = cur;
   w.cur2 = cur2;
+  w.cur3 = cur3;
+  w.cur4 = cur4;
   w.max_len = p < p1 ? ((p1 - p) < 258 ? (p1 - p) : 258) : 0;
   w.best_len = 0;
   w.best_dist = 0;
@@ -306,70 +322,78 @@ __device__ __forceinline__ void walk_init(Walk &w, const MatchShared *s, const D
   w.hops = 0;
   w.max_hops = (int)w.best_len >= P.good ? (P.max_chain >> 2) : P.max_chain;
   w.active = w.max_len >= (uint32_t)P.klen && (int)w.best_len < P.skip_len;
+  // one word per hop filters the candidates: the word ending at best_len (a
+  // candidate can only win if it matches there), or before any match the
+  // first bytes of the key (the chains' hash buckets also hold collisions)
   w.o = w.best_len >= 4 ? w.best_len - 3 : 0;
-  w.pw = 0;
+  w.omask = w.best_len >= 4 || P.klen >= 4 ? 0xFFFFFFFFu : 0xFFFFFFu;
+  w.pw = cur;
   w.link = 0;
   if (w.active) {
-    // the word ending at best_len: a candidate can only win if it matches there
-    w.pw = w.best_len >= 4 ? ld32(s, p + w.o) : 0u;
+    if (w.best_len >= 4) w.pw = ld32(s, p + w.o);
     w.link = s->prev[ridx(p)];
     w.active = w.link != 0;
   }
 }
 
-// a candidate q that passed the key checks: extend and keep the longest
+// a candidate q that passed the one-word filter: its length from byte 0
+// (the filter checked at most 4 bytes) and keep the longest
 __device__ __forceinline__ void walk_extend(Walk &w, const MatchShared *s, const DeflateParams &P, uint32_t q) {
 #ifdef ZT_DF_COUNT
   atomicAdd(&g_df_count[2], 1ull);
 #endif
-  uint32_t len = (uint32_t)P.klen;
+  uint32_t len;
   {
-    // the next 16 bytes in one round of loads (most matches end there)
-    const uint32_t x0 = ld32(s, q + len) ^ ld32(s, w.p + len);
-    const uint32_t x1 = ld32(s, q + len + 4) ^ ld32(s, w.p + len + 4);
-    const uint32_t x2 = ld32(s, q + len + 8) ^ ld32(s, w.p + len + 8);
-    const uint32_t x3 = ld32(s, q + len + 12) ^ ld32(s, w.p + len + 12);
+    // the first 16 bytes: q's words in one run of loads, p's from registers
+    uint32_t qw[4];
+    ld_run<4>(s, q, qw);
+    const uint32_t x0 = qw[0] ^ w.cur, x1 = qw[1] ^ w.cur2, x2 = qw[2] ^ w.cur3, x3 = qw[3] ^ w.cur4;
+    if (x0) len = (uint32_t)(__ffs(x0) - 1) >> 3;
+    else if (x1) len = 4 + ((uint32_t)(__ffs(x1) - 1) >> 3);
+    else if (x2) len = 8 + ((uint32_t)(__ffs(x2) - 1) >> 3);
+    else if (x3) len = 12 + ((uint32_t)(__ffs(x3) - 1) >> 3);
+    else len = 16;
+  }
+  // all 16 matched: 16 more bytes per round until a mismatch (or max_len)
+  bool more = len == 16;
+  while (more && len < w.max_len) {
+    uint32_t qw[4], pw[4];
+    ld_run<4>(s, q + len, qw);
+    ld_run<4>(s, w.p + len, pw);
+    const uint32_t x0 = qw[0] ^ pw[0], x1 = qw[1] ^ pw[1], x2 = qw[2] ^ pw[2], x3 = qw[3] ^ pw[3];
     if (x0) len += (uint32_t)(__ffs(x0) - 1) >> 3;
     else if (x1) len += 4 + ((uint32_t)(__ffs(x1) - 1) >> 3);
     else if (x2) len += 8 + ((uint32_t)(__ffs(x2) - 1) >> 3);
     else if (x3) len += 12 + ((uint32_t)(__ffs(x3) - 1) >> 3);
-    else len += 16;
-  }
-  const bool more = len == (uint32_t)P.klen + 16;
-  while (more && len < w.max_len) {
-    // all 16 matched: continue 4 bytes at a time
-    const uint32_t x = ld32(s, q + len) ^ ld32(s, w.p + len);
-    if (x) {
-      len += (uint32_t)(__ffs(x) - 1) >> 3;
-      break;
-    }
-    len += 4;
+    more = (x0 | x1 | x2 | x3) == 0;
+    if (more) len += 16;
   }
   if (len > w.max_len) len = w.max_len;
-  if (len > w.best_len) {
+  if (len >= 3 && len > w.best_len) {
     w.best_len = len;
     w.best_dist = w.p - q;
     if ((int)len >= P.nice_len || len >= w.max_len) {
       w.active = false;
       return;
     }
-    w.o = len - 3;
-    w.pw = ld32(s, w.p + w.o);
+    if (len >= 4) {
+      w.o = len - 3;
+      w.omask = 0xFFFFFFFFu;
+      w.pw = ld32(s, w.p + w.o);
+    }
   }
 }
 
 // one hop of two walks: every LDS load of both hops is issued before any is
-// used (the walks are latency-bound pointer chases), then the checks
-__device__ __forceinline__ void walk_pair_step(Walk &a, Walk &b, const MatchShared *s, const DeflateParams &P,
-                                               Key key) {
+// used (the walks are latency-bound pointer chases), then the checks.  Per
+// hop two loads: the link and the filter word.
+__device__ __forceinline__ void walk_pair_step(Walk &a, Walk &b, const MatchShared *s, const DeflateParams &P) {
   const uint32_t qa = a.active ? a.q - a.link : a.q;
   const uint32_t qb = b.active ? b.q - b.link : b.q;
   const bool ha = a.active && a.p - qa <= (uint32_t)DF_MAXDIST;
   const bool hb = b.active && b.p - qb <= (uint32_t)DF_MAXDIST;
   const uint32_t la = s->prev[ridx(qa)], lb = s->prev[ridx(qb)];
   const uint32_t oa = ld32(s, qa + a.o), ob = ld32(s, qb + b.o);
-  const uint32_t ka = ld32(s, qa), kb = ld32(s, qb);
-  const uint32_t ka2 = ld32(s, qa + 4), kb2 = ld32(s, qb + 4);
   a.q = qa;
   b.q = qb;
   a.hops += ha ? 1 : 0;
@@ -378,10 +402,8 @@ __device__ __forceinline__ void walk_pair_step(Walk &a, Walk &b, const MatchShar
   if ((threadIdx.x & 63) == 0) atomicAdd(&g_df_count[0], 1ull);
   atomicAdd(&g_df_count[1], (unsigned long long)(ha ? 1 : 0) + (hb ? 1 : 0));
 #endif
-  const bool ca = ha && (a.best_len < 4 || oa == a.pw) && ((ka ^ a.cur) & key.kmask) == 0 &&
-                  ((ka2 ^ a.cur2) & key.kmask2) == 0;
-  const bool cb = hb && (b.best_len < 4 || ob == b.pw) && ((kb ^ b.cur) & key.kmask) == 0 &&
-                  ((kb2 ^ b.cur2) & key.kmask2) == 0;
+  const bool ca = ha && ((oa ^ a.pw) & a.omask) == 0;
+  const bool cb = hb && ((ob ^ b.pw) & b.omask) == 0;
   a.link = la;
   b.link = lb;
   a.active = ha && la != 0 && a.hops < a.max_hops;
@@ -392,7 +414,7 @@ __device__ __forceinline__ void walk_pair_step(Walk &a, Walk &b, const MatchShar
 
 // finish position pb + K: near probes when the chain found nothing long
 template <int K>
-__device__ __forceinline__ uint32_t walk_finish(const Walk &w, const DeflateParams &P, const uint32_t (&win)[8],
+__device__ __forceinline__ uint32_t walk_finish(const Walk &w, const DeflateParams &P, const uint32_t (&win)[9],
                                                 uint32_t near, uint32_t &carry_len, uint32_t &carry_dist) {
   uint32_t best_len = w.best_len, best_dist = w.best_dist;
   if (near == 0 && w.max_len >= 3 && best_len < (uint32_t)P.klen)
@@ -407,25 +429,25 @@ __device__ __forceinline__ uint32_t walk_finish(const Walk &w, const DeflatePara
 __device__ void search_quad(const MatchShared *s, const DeflateParams &P, uint32_t pb, uint32_t p0, uint32_t p1,
                             Key key, uint32_t *res_out) {
   if (pb >= p1) return;
-  // bytes [pb - 16, pb + 16) (pb is a multiple of 4; before rel 0 the words
+  // bytes [pb - 16, pb + 20) (pb is a multiple of 4; before rel 0 the words
   // are never used: near distances stay <= p)
-  uint32_t w[8];
+  uint32_t w[9];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) w[i] = s->ring[ridx(pb - 16 + 4 * i) >> 2];
+  for (int i = 0; i < 9; ++i) w[i] = s->ring[ridx(pb - 16 + 4 * i) >> 2];
   // positions 0 and 2 walk together, then 1 and 3 with the carry of 0 and 2
   uint32_t out[4];
   uint32_t c0l, c0d, c2l, c2d, cl, cd;
   const uint32_t nr0 = near_any<0, 1>(w, win32<16>(w), ~0u), nr1 = near_any<1, 1>(w, win32<17>(w), ~0u);
   const uint32_t nr2 = near_any<2, 1>(w, win32<18>(w), ~0u), nr3 = near_any<3, 1>(w, win32<19>(w), ~0u);
   Walk wa, wb;
-  walk_init(wa, s, P, pb, p1, win32<16>(w), win32<20>(w), 0, 0);
-  walk_init(wb, s, P, pb + 2, p1, win32<18>(w), win32<22>(w), 0, 0);
-  while (wa.active || wb.active) walk_pair_step(wa, wb, s, P, key);
+  walk_init(wa, s, P, pb, p1, win32<16>(w), win32<20>(w), win32<24>(w), win32<28>(w), 0, 0);
+  walk_init(wb, s, P, pb + 2, p1, win32<18>(w), win32<22>(w), win32<26>(w), win32<30>(w), 0, 0);
+  while (wa.active || wb.active) walk_pair_step(wa, wb, s, P);
   out[0] = walk_finish<0>(wa, P, w, nr0, c0l, c0d);
   out[2] = walk_finish<2>(wb, P, w, nr2, c2l, c2d);
-  walk_init(wa, s, P, pb + 1, p1, win32<17>(w), win32<21>(w), c0l, c0d);
-  walk_init(wb, s, P, pb + 3, p1, win32<19>(w), win32<23>(w), c2l, c2d);
-  while (wa.active || wb.active) walk_pair_step(wa, wb, s, P, key);
+  walk_init(wa, s, P, pb + 1, p1, win32<17>(w), win32<21>(w), win32<25>(w), win32<29>(w), c0l, c0d);
+  walk_init(wb, s, P, pb + 3, p1, win32<19>(w), win32<23>(w), win32<27>(w), win32<31>(w), c2l, c2d);
+  while (wa.active || wb.active) walk_pair_step(wa, wb, s, P);
   out[1] = walk_finish<1>(wa, P, w, nr1, cl, cd);
   out[3] = walk_finish<3>(wb, P, w, nr3, cl, cd);
   if (pb + 4 <= p1) {
