@@ -13,5 +13,5 @@ grep metric gpurun_out/${TAG}_bench.log | python3 -c "import json,sys; d=json.lo
 python3 - <<PY
 import csv
 rows=list(csv.DictReader(open('gpurun_out/${TAG}_prof/run_kernel_stats.csv')))
-for r in rows[:12]: print('%-40s %4s %10.3f ms' % (r['Name'].split('(')[0].split('::')[-1][:40], r['Calls'], float(r['AverageNs'])/1e6))
+for r in rows[:12]: print('%-40s %4s %10.3f ms' % (r['Name'].replace('zt::(anonymous namespace)::','').split('(')[0][:40], r['Calls'], float(r['AverageNs'])/1e6))
 PY

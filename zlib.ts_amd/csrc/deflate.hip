@@ -40,6 +40,7 @@ namespace zt {
 
 #ifdef ZT_DF_TIME
 __device__ unsigned long long g_df_time[8];  // debug: cycles (thread 0 of each workgroup) in phases
+__device__ unsigned long long g_bk_time[8];  // debug: block_kernel phase cycles (lane 0), [6] = blocks
 #define DF_T(v) v = __builtin_readcyclecounter()
 #else
 #define DF_T(v) (void)0
@@ -557,18 +558,32 @@ struct HufScratch {
   uint32_t bl_count[40];
 };
 
+// parse staging ring (parse_block_dma)
+constexpr int PB_CH = 4;
+constexpr int PB_NCH = 5;
+constexpr int PB_LOADS = PB_CH + PB_CH / 4;  // global_load_lds per chunk (res words, then data words)
+struct ParseStage {
+  uint32_t res[PB_NCH][PB_CH * 64];
+  uint32_t byt[PB_NCH][PB_CH * 16];
+};
+
 struct BlockShared {
   uint32_t lit_hist[288];
   uint32_t dist_hist[32];
-  uint32_t lit_code[288];
-  uint32_t dist_code[32];
-  uint32_t cl_code[19];
-  uint8_t lit_len[288];
-  uint8_t dist_len[32];
-  uint8_t cl_len[20];
-  uint16_t cl_syms[320];  // sym | extra_value << 5
   uint32_t n_cl_syms, hlit, hdist, hclen;
-  HufScratch huf;
+  union {
+    ParseStage stage;  // the parse's staging ring, then the code construction
+    struct {
+      uint32_t lit_code[288];
+      uint32_t dist_code[32];
+      uint32_t cl_code[19];
+      uint8_t lit_len[288];
+      uint8_t dist_len[32];
+      uint8_t cl_len[20];
+      uint16_t cl_syms[320];  // sym | extra_value << 5
+      HufScratch huf;
+    };
+  };
 };
 
 // One wave per workgroup: LDS operations of a wave complete in order, so a
@@ -792,11 +807,100 @@ struct HdrOut {
   }
 };
 
-// parse (pointer doubling over 64-position windows) -> tokens over res, histograms
+// LDS histogram increment as inline asm: the compiler puts an
+// s_waitcnt vmcnt(0) before every LDS store it sees while LDS-DMA loads are in
+// flight (it cannot tell the parse ring from the histograms), which would
+// drain parse_block_dma's prefetch at every window.  (LDS operations complete
+// in order, so the compiler's own lgkmcnt waits stay sufficient.)
+__device__ __forceinline__ void lds_inc(uint32_t *p) {
+  const uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t *)p;
+  __asm__ volatile("ds_add_u32 %0, %1" ::"v"(a), "v"(1u) : "memory");
+}
+
+// parse -> tokens over res, histograms.  One 64-position window per step:
+// the path through it from `entry` (a scalar walk over the match lanes, or
+// pointer doubling when they are many), its tokens written in order.
 // (WRITE = false: histograms of the greedy parse only, res untouched)
+template <bool WRITE, class S>
+__device__ __forceinline__ void parse_window(S *s, const DeflateParams &P, uint32_t *r_blk, uint32_t len, uint32_t w0,
+                                             uint32_t r, uint32_t byte, uint32_t r_next, uint32_t &entry,
+                                             uint32_t &ntok) {
+  const int lane = threadIdx.x & 63;
+    const uint32_t i = w0 + lane;
+    uint32_t L = r >> 16;
+    if (P.lazy && !P.opt) {
+      // one-step lazy: a longer match at i + 1 defers this one
+      uint32_t nb = (uint32_t)__shfl_down((int)r, 1, 64) >> 16;
+      const uint32_t first_next = (uint32_t)__shfl((int)r_next, 0, 64) >> 16;
+      if (lane == 63) nb = first_next;
+      if (L >= 3 && i + 1 < len && nb > L) L = 0;
+    }
+    // the path through the window.  Few match lanes past the entry: a scalar
+    // walk (literal runs up to the next match lane, then a jump past it);
+    // many: pointer doubling (6 rounds of lane shuffles)
+    const uint64_t valid = __ballot(i < len);
+    const uint64_t mm = __ballot(i < len && L >= 3);
+    uint64_t path = 0;
+    uint32_t exit;
+    if (__popcll(mm & (~0ull << entry)) <= 3) {
+      uint32_t cur = entry;
+      while (cur < 64) {
+        const uint64_t rest = mm & (~0ull << cur);
+        const uint32_t m = rest ? (uint32_t)__builtin_ctzll(rest) : 64u;
+        path |= (m >= 64 ? ~0ull : ((1ull << m) - 1)) & (~0ull << cur);
+        if (m >= 64) {
+          cur = 64;
+          break;
+        }
+        path |= 1ull << m;
+        cur = m + (uint32_t)__builtin_amdgcn_readlane((int)L, (int)m);
+      }
+      path &= valid;
+      exit = cur;
+    } else {
+      const uint32_t step = L >= 3 ? L : 1;
+      uint32_t ptr = i < len ? lane + step : 64u;
+      uint64_t mask = i < len ? 1ull << lane : 0ull;
+#pragma unroll
+      for (int rnd = 0; rnd < 6; ++rnd) {
+        const bool in = ptr < 64;
+        const int src = in ? (int)ptr : lane;
+        uint32_t mlo = __shfl((uint32_t)mask, src, 64);
+        uint32_t mhi = __shfl((uint32_t)(mask >> 32), src, 64);
+        uint32_t nptr = __shfl(ptr, src, 64);
+        if (in) {
+          mask |= ((uint64_t)mhi << 32) | mlo;
+          ptr = nptr;
+        }
+      }
+      // (readlane returns int: go through uint32_t so the low half is not sign-extended)
+      const uint32_t path_hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(mask >> 32), (int)entry);
+      const uint32_t path_lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mask, (int)entry);
+      path = ((uint64_t)path_hi << 32) | path_lo;
+      exit = (uint32_t)__builtin_amdgcn_readlane((int)ptr, (int)entry);
+    }
+    const bool on = (path >> lane) & 1;
+    if (on) {
+      uint32_t token;
+      if (L >= 3) {
+        token = (L << 16) | (r & 0xFFFF);
+        uint32_t eb, ev;
+        lds_inc(&s->lit_hist[257 + len_sym(L)]);
+        lds_inc(&s->dist_hist[dist_sym(r & 0xFFFF, eb, ev)]);
+      } else {
+        token = byte;
+        lds_inc(&s->lit_hist[token]);
+      }
+      if (WRITE) r_blk[ntok + __popcll(path & lanemask_lt(lane))] = token;
+    }
+    ntok += __popcll(path);
+    entry = exit - 64;
+}
+
+// register-prefetch driver (any alignment / length)
 constexpr int PB_PF = 6;  // parse windows prefetched
 template <bool WRITE, class S>
-__device__ uint32_t parse_block(S *s, const DeflateParams &P, uint32_t *r_blk, const uint8_t *data, uint32_t len) {
+__device__ uint32_t parse_block_regs(S *s, const DeflateParams &P, uint32_t *r_blk, const uint8_t *data, uint32_t len) {
   const int lane = threadIdx.x & 63;
   uint32_t entry = 0;  // first path position relative to the current window
   uint32_t ntok = 0;
@@ -812,67 +916,83 @@ __device__ uint32_t parse_block(S *s, const DeflateParams &P, uint32_t *r_blk, c
   for (uint32_t wb = 0; wb < len; wb += 64 * PB_PF) {
 #pragma unroll
     for (int j = 0; j < PB_PF; ++j) {
-    const uint32_t w0 = wb + 64u * j;
-    if (w0 >= len) break;
-    const uint32_t r = rq[j], byte = bq[j];
-    {
-      const uint32_t p = w0 + 64u * PB_PF + lane;
-      rq[j] = p < len ? r_blk[p] : 0u;
-      bq[j] = p < len ? data[p] : 0u;
-    }
-    const uint32_t r_next = rq[(j + 1) % PB_PF];
-    if (entry >= 64) {
-      entry -= 64;
-      continue;
-    }
-    const uint32_t i = w0 + lane;
-    uint32_t L = r >> 16;
-    if (P.lazy && !P.opt) {
-      // one-step lazy: a longer match at i + 1 defers this one
-      uint32_t nb = (uint32_t)__shfl_down((int)r, 1, 64) >> 16;
-      const uint32_t first_next = (uint32_t)__shfl((int)r_next, 0, 64) >> 16;
-      if (lane == 63) nb = first_next;
-      if (L >= 3 && i + 1 < len && nb > L) L = 0;
-    }
-    const uint32_t step = L >= 3 ? L : 1;
-    uint32_t ptr = i < len ? lane + step : 64u;
-    uint64_t mask = i < len ? 1ull << lane : 0ull;
-#pragma unroll
-    for (int rnd = 0; rnd < 6; ++rnd) {
-      const bool in = ptr < 64;
-      const int src = in ? (int)ptr : lane;
-      uint32_t mlo = __shfl((uint32_t)mask, src, 64);
-      uint32_t mhi = __shfl((uint32_t)(mask >> 32), src, 64);
-      uint32_t nptr = __shfl(ptr, src, 64);
-      if (in) {
-        mask |= ((uint64_t)mhi << 32) | mlo;
-        ptr = nptr;
+      const uint32_t w0 = wb + 64u * j;
+      if (w0 >= len) break;
+      const uint32_t r = rq[j], byte = bq[j];
+      {
+        const uint32_t p = w0 + 64u * PB_PF + lane;
+        rq[j] = p < len ? r_blk[p] : 0u;
+        bq[j] = p < len ? data[p] : 0u;
       }
-    }
-    // (readlane returns int: go through uint32_t so the low half is not sign-extended)
-    const uint32_t path_hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(mask >> 32), (int)entry);
-    const uint32_t path_lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mask, (int)entry);
-    const uint64_t path = ((uint64_t)path_hi << 32) | path_lo;
-    const uint32_t exit = (uint32_t)__builtin_amdgcn_readlane((int)ptr, (int)entry);
-    const bool on = (path >> lane) & 1;
-    if (on) {
-      uint32_t token;
-      if (L >= 3) {
-        token = (L << 16) | (r & 0xFFFF);
-        uint32_t eb, ev;
-        atomicAdd(&s->lit_hist[257 + len_sym(L)], 1u);
-        atomicAdd(&s->dist_hist[dist_sym(r & 0xFFFF, eb, ev)], 1u);
-      } else {
-        token = byte;
-        atomicAdd(&s->lit_hist[token], 1u);
+      const uint32_t r_next = rq[(j + 1) % PB_PF];
+      if (entry >= 64) {
+        entry -= 64;
+        continue;
       }
-      if (WRITE) r_blk[ntok + __popcll(path & lanemask_lt(lane))] = token;
-    }
-    ntok += __popcll(path);
-    entry = exit - 64;
+      parse_window<WRITE>(s, P, r_blk, len, w0, r, byte, r_next, entry, ntok);
     }
   }
   return ntok;
+}
+
+// LDS-DMA driver for whole, 4-byte aligned blocks: chunks of PB_CH windows
+// (res words and data bytes) stream into a ring of PB_NCH chunks by
+// global_load_lds, PB_NCH - 1 chunks ahead, with one counted vmcnt wait per
+// chunk -- the register driver's loads could not stay in flight across the
+// window loop's branches (the compiler waited for each window's loads).
+__device__ __forceinline__ void vm_wait_loads(void) {
+  // vmcnt(PB_LOADS * (PB_NCH - 2)): chunks c and c + 1 have landed (loads
+  // complete in order; stores in between only make this wait longer)
+  constexpr int N = PB_LOADS * (PB_NCH - 2);
+  static_assert(N < 64, "vmcnt field");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0F70);
+}
+template <bool WRITE, class S>
+__device__ uint32_t parse_block_dma(S *s, ParseStage *st, const DeflateParams &P, uint32_t *r_blk, const uint8_t *data) {
+  const int lane = threadIdx.x & 63;
+  constexpr uint32_t nch = DF_BLOCK / (PB_CH * 64);
+  auto issue = [&](uint32_t c) {
+    // past the block: re-read chunk 0 (the count of loads stays fixed)
+    const uint32_t cc = c < nch ? c : 0u;
+    const uint32_t slot = c % PB_NCH;
+#pragma unroll
+    for (int w = 0; w < PB_CH; ++w)
+      __builtin_amdgcn_global_load_lds(r_blk + cc * (PB_CH * 64) + w * 64 + lane, &st->res[slot][w * 64], 4, 0, 0);
+#pragma unroll
+    for (int w = 0; w < PB_CH / 4; ++w)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint32_t *>(data + cc * (PB_CH * 64) + w * 256) + lane,
+                                       &st->byt[slot][w * 64], 4, 0, 0);
+  };
+#pragma unroll
+  for (int c = 0; c < PB_NCH - 1; ++c) issue((uint32_t)c);
+  uint32_t entry = 0, ntok = 0;
+  for (uint32_t c = 0; c < nch; ++c) {
+    issue(c + PB_NCH - 1);
+    vm_wait_loads();
+    const uint32_t slot = c % PB_NCH, nslot = (c + 1) % PB_NCH;
+    const uint8_t *bytes = reinterpret_cast<const uint8_t *>(st->byt[slot]);
+    for (int w = 0; w < PB_CH; ++w) {
+      const uint32_t w0 = c * (PB_CH * 64) + (uint32_t)w * 64;
+      if (entry >= 64) {
+        entry -= 64;
+        continue;
+      }
+      const uint32_t r = st->res[slot][w * 64 + lane];
+      const uint32_t byte = bytes[w * 64 + lane];
+      const uint32_t r_next = w + 1 < PB_CH ? st->res[slot][(w + 1) * 64] : st->res[nslot][0];
+      parse_window<WRITE>(s, P, r_blk, DF_BLOCK, w0, r, byte, r_next, entry, ntok);
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): no DMA into the ring after return
+  return ntok;
+}
+
+template <bool WRITE, class S>
+__device__ uint32_t parse_block(S *s, ParseStage *st, const DeflateParams &P, uint32_t *r_blk, const uint8_t *data,
+                                uint32_t len) {
+  if (len == DF_BLOCK && (reinterpret_cast<uintptr_t>(data) & 3) == 0)
+    return parse_block_dma<WRITE>(s, st, P, r_blk, data);
+  return parse_block_regs<WRITE>(s, P, r_blk, data, len);
 }
 
 // ================================ 1b. optparse_kernel ================================
@@ -909,6 +1029,7 @@ struct BlockPrices {
 struct PriceShared {
   uint32_t lit_hist[288];
   uint32_t dist_hist[32];
+  ParseStage stage;
 };
 
 __device__ __forceinline__ uint32_t op_price(uint32_t f, float inv_total) {
@@ -930,7 +1051,7 @@ __global__ __launch_bounds__(64) void price_kernel(DeflateParams P) {
   for (int i = lane; i < 288; i += 64) s->lit_hist[i] = 0;
   if (lane < 32) s->dist_hist[lane] = 0;
   wsync();
-  parse_block<false>(s, P, P.res + lo, P.base + P.halo + lo, blen);
+  parse_block<false>(s, &s->stage, P, P.res + lo, P.base + P.halo + lo, blen);
   wsync();
   BlockPrices *bp = reinterpret_cast<BlockPrices *>(P.slots + (size_t)blk * DF_SLOT);
   float tl = 0.f, td = 0.f;
@@ -1111,12 +1232,23 @@ __global__ __launch_bounds__(64) void block_kernel(DeflateParams P) {
   for (int i = lane; i < 288; i += 64) s->lit_hist[i] = 0;
   if (lane < 32) s->dist_hist[lane] = 0;
   wsync();
-  const uint32_t ntok = parse_block<true>(s, P, r_blk, data, blen);
+#ifdef ZT_DF_TIME
+  uint64_t bt0 = __builtin_readcyclecounter(), btk;
+#define BK_T(k)                                                                          \
+  btk = __builtin_readcyclecounter();                                                    \
+  if (lane == 0) atomicAdd(&g_bk_time[k], (unsigned long long)(btk - bt0));              \
+  bt0 = btk;
+#else
+#define BK_T(k) (void)0
+#endif
+  const uint32_t ntok = parse_block<true>(s, &s->stage, P, r_blk, data, blen);
+  BK_T(0);
   wsync();
   if (lane == 0) s->lit_hist[256] += 1;  // end of block
   wsync();
   huff_lengths(s, s->lit_hist, 286, 15, s->lit_len);
   huff_lengths(s, s->dist_hist, 30, 15, s->dist_len);
+  BK_T(1);
   if (lane == 0) {
     uint32_t hlit = 286, hdist = 30;
     while (hlit > 257 && s->lit_len[hlit - 1] == 0) --hlit;
@@ -1170,10 +1302,12 @@ __global__ __launch_bounds__(64) void block_kernel(DeflateParams P) {
     for (int k = 0; k < 19; ++k) s->cl_code[k] = clf[k];
   }
   wsync();
+  BK_T(2);
   huff_lengths(s, s->cl_code, 19, 7, s->cl_len);
   huff_codes(s->lit_len, 286, s->lit_code);
   huff_codes(s->dist_len, 30, s->dist_code);
   huff_codes(s->cl_len, 19, s->cl_code);
+  BK_T(3);
   // sizes of the three choices (bits, without the sync marker)
   uint64_t dyn = 0, fix = 0;
   for (int i = lane; i < 286; i += 64) {
@@ -1208,6 +1342,7 @@ __global__ __launch_bounds__(64) void block_kernel(DeflateParams P) {
   const uint64_t stored_bits = 8ull * (blen + 10);  // + its sync point
   const uint64_t dyn_bits = ((dyn + 3 + 7) & ~7ull) + 32;
   const uint64_t fix_bits = ((fix + 3 + 7) & ~7ull) + 32;
+  BK_T(4);
   uint32_t bt;
   if (P.ctype == 1) bt = 1;
   else if (stored_bits <= dyn_bits && stored_bits <= fix_bits) bt = 0;
@@ -1246,6 +1381,11 @@ __global__ __launch_bounds__(64) void block_kernel(DeflateParams P) {
     plan->blen = blen;
     plan->last = last ? 1 : 0;
   }
+  BK_T(5);
+#ifdef ZT_DF_TIME
+  if (lane == 0) atomicAdd(&g_bk_time[6], 1ull);
+#endif
+#undef BK_T
 }
 
 // ================================ 3. encode_kernel ================================
@@ -1686,6 +1826,15 @@ extern "C" int zt_debug_df_time(unsigned long long *out) {
   (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_df_time), sizeof(unsigned long long) * 8);
   unsigned long long z[8] = {};
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_df_time), z, sizeof z);
+  return 0;
+}
+#endif
+
+#ifdef ZT_DF_TIME
+extern "C" int zt_debug_bk_time(unsigned long long *out) {
+  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bk_time), sizeof(unsigned long long) * 8);
+  unsigned long long z[8] = {};
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_bk_time), z, sizeof z);
   return 0;
 }
 #endif
