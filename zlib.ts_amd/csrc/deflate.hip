@@ -337,37 +337,35 @@ __device__ __forceinline__ void walk_init(Walk &w, const MatchShared *s, const D
   }
 }
 
+// equal leading bytes (0..16) of four XORed words, without branches
+__device__ __forceinline__ uint32_t eq_len16(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) {
+  const uint32_t l0 = min((uint32_t)(__ffs(x0) - 1) >> 3, 4u), l1 = min((uint32_t)(__ffs(x1) - 1) >> 3, 4u);
+  const uint32_t l2 = min((uint32_t)(__ffs(x2) - 1) >> 3, 4u), l3 = min((uint32_t)(__ffs(x3) - 1) >> 3, 4u);
+  const uint32_t t2 = l2 == 4 ? 4 + l3 : l2;
+  const uint32_t t1 = l1 == 4 ? 4 + t2 : l1;
+  return l0 == 4 ? 4 + t1 : l0;
+}
+
 // a candidate q that passed the one-word filter: its length from byte 0
 // (the filter checked at most 4 bytes) and keep the longest
 __device__ __forceinline__ void walk_extend(Walk &w, const MatchShared *s, const DeflateParams &P, uint32_t q) {
 #ifdef ZT_DF_COUNT
   atomicAdd(&g_df_count[2], 1ull);
 #endif
-  uint32_t len;
-  {
-    // the first 16 bytes: q's words in one run of loads, p's from registers
-    uint32_t qw[4];
-    ld_run<4>(s, q, qw);
-    const uint32_t x0 = qw[0] ^ w.cur, x1 = qw[1] ^ w.cur2, x2 = qw[2] ^ w.cur3, x3 = qw[3] ^ w.cur4;
-    if (x0) len = (uint32_t)(__ffs(x0) - 1) >> 3;
-    else if (x1) len = 4 + ((uint32_t)(__ffs(x1) - 1) >> 3);
-    else if (x2) len = 8 + ((uint32_t)(__ffs(x2) - 1) >> 3);
-    else if (x3) len = 12 + ((uint32_t)(__ffs(x3) - 1) >> 3);
-    else len = 16;
-  }
+  // the first 16 bytes: q's words in one run of loads, p's from registers;
+  // lengths branch-free, so that every load of the run is in flight at once
+  uint32_t qw[4];
+  ld_run<4>(s, q, qw);
+  uint32_t len = eq_len16(qw[0] ^ w.cur, qw[1] ^ w.cur2, qw[2] ^ w.cur3, qw[3] ^ w.cur4);
   // all 16 matched: 16 more bytes per round until a mismatch (or max_len)
   bool more = len == 16;
   while (more && len < w.max_len) {
-    uint32_t qw[4], pw[4];
-    ld_run<4>(s, q + len, qw);
-    ld_run<4>(s, w.p + len, pw);
-    const uint32_t x0 = qw[0] ^ pw[0], x1 = qw[1] ^ pw[1], x2 = qw[2] ^ pw[2], x3 = qw[3] ^ pw[3];
-    if (x0) len += (uint32_t)(__ffs(x0) - 1) >> 3;
-    else if (x1) len += 4 + ((uint32_t)(__ffs(x1) - 1) >> 3);
-    else if (x2) len += 8 + ((uint32_t)(__ffs(x2) - 1) >> 3);
-    else if (x3) len += 12 + ((uint32_t)(__ffs(x3) - 1) >> 3);
-    more = (x0 | x1 | x2 | x3) == 0;
-    if (more) len += 16;
+    uint32_t qx[4], px[4];
+    ld_run<4>(s, q + len, qx);
+    ld_run<4>(s, w.p + len, px);
+    const uint32_t l = eq_len16(qx[0] ^ px[0], qx[1] ^ px[1], qx[2] ^ px[2], qx[3] ^ px[3]);
+    len += l;
+    more = l == 16;
   }
   if (len > w.max_len) len = w.max_len;
   if (len >= 3 && len > w.best_len) {
