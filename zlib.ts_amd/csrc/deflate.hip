@@ -1005,13 +1005,17 @@ __device__ uint32_t parse_block(S *s, ParseStage *st, const DeflateParams &P, ui
 // res[i] (0 = literal), so the block kernel's parse follows the DP's path.
 // Every value left in res is a valid (shorter or equal) match, so the stream
 // stays correct whatever the cost model says.
-// C is kept modulo 2^16 in a 260-row LDS ring per lane (row = step mod 260,
+// C is kept modulo 2^16 in an OP_RING-row LDS ring per lane (row = step mod OP_RING,
 // all lanes on the same row at the same step, so reads of one length l hit
 // distinct banks): differences over <= 258 positions stay below 2^15.
 typedef unsigned int op_u32x4 __attribute__((ext_vector_type(4)));
 constexpr int OP_SEG = 512;
 constexpr int OP_OV = 128;
-constexpr int OP_RING = 260;
+// C ring rows: C[i + l] for l <= OP_RING.  A longer match reads C[i + OP_RING]
+// instead of C[i + L] (an estimate of its continuation: the parse stays
+// valid, only the DP's cost model is approximate there); 132 rows keep the
+// LDS at 17 KiB per wave (9 waves per CU instead of 4 at 260 rows)
+constexpr int OP_RING = 132;
 constexpr int OP_SHORT = 16;
 constexpr int OP_PF = 4;      // groups of 16 positions prefetched per lane  // every cut length 3..OP_SHORT is tried, longer ones only at L
 
@@ -1172,7 +1176,8 @@ __global__ __launch_bounds__(64) void optparse_kernel(DeflateParams P) {
               const uint32_t Dc = D ? D : 1u;
               const int dc = (int)s->pr.distc[dist_sym(Dc, eb, ev)];
               const uint32_t Lc = L < 3 ? 3u : L;
-              const uint32_t rr = row >= Lc ? row - Lc : row + OP_RING - Lc;
+              const uint32_t Lr = Lc < (uint32_t)OP_RING ? Lc : (uint32_t)OP_RING;
+              const uint32_t rr = row >= Lr ? row - Lr : row + OP_RING - Lr;
               const int c_far = (int)(int16_t)(uint16_t)(s->ring[rr][lane] - (uint16_t)C1) + (int)s->pr.lenc[Lc];
               const int lit = live ? (int)s->pr.litc[(bv >> (8 * (k & 3))) & 0xFF] : 0;
               uint32_t key = (uint32_t)(lit + 0x8000) << 9;
