@@ -883,13 +883,19 @@ __device__ __forceinline__ void parse_window(S *s, const DeflateParams &P, uint3
       if (L >= 3) {
         token = (L << 16) | (r & 0xFFFF);
         uint32_t eb, ev;
+#ifndef ZT_EXP_NOHIST
         lds_inc(&s->lit_hist[257 + len_sym(L)]);
         lds_inc(&s->dist_hist[dist_sym(r & 0xFFFF, eb, ev)]);
+#endif
       } else {
         token = byte;
+#ifndef ZT_EXP_NOHIST
         lds_inc(&s->lit_hist[token]);
+#endif
       }
+#ifndef ZT_EXP_NOSTORE
       if (WRITE) r_blk[ntok + __popcll(path & lanemask_lt(lane))] = token;
+#endif
     }
     ntok += __popcll(path);
     entry = exit - 64;
@@ -946,9 +952,10 @@ __device__ __forceinline__ void vm_wait_loads(void) {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0F70);
 }
 template <bool WRITE, class S>
-__device__ uint32_t parse_block_dma(S *s, ParseStage *st, const DeflateParams &P, uint32_t *r_blk, const uint8_t *data) {
+__device__ uint32_t parse_block_dma(S *s, ParseStage *st, const DeflateParams &P, uint32_t *r_blk, const uint8_t *data,
+                                    uint32_t len) {
   const int lane = threadIdx.x & 63;
-  constexpr uint32_t nch = DF_BLOCK / (PB_CH * 64);
+  const uint32_t nch = len / (PB_CH * 64);  // len: a multiple of PB_CH * 64
   auto issue = [&](uint32_t c) {
     // past the block: re-read chunk 0 (the count of loads stays fixed)
     const uint32_t cc = c < nch ? c : 0u;
@@ -978,7 +985,7 @@ __device__ uint32_t parse_block_dma(S *s, ParseStage *st, const DeflateParams &P
       const uint32_t r = st->res[slot][w * 64 + lane];
       const uint32_t byte = bytes[w * 64 + lane];
       const uint32_t r_next = w + 1 < PB_CH ? st->res[slot][(w + 1) * 64] : st->res[nslot][0];
-      parse_window<WRITE>(s, P, r_blk, DF_BLOCK, w0, r, byte, r_next, entry, ntok);
+      parse_window<WRITE>(s, P, r_blk, len, w0, r, byte, r_next, entry, ntok);
     }
   }
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): no DMA into the ring after return
@@ -988,8 +995,8 @@ __device__ uint32_t parse_block_dma(S *s, ParseStage *st, const DeflateParams &P
 template <bool WRITE, class S>
 __device__ uint32_t parse_block(S *s, ParseStage *st, const DeflateParams &P, uint32_t *r_blk, const uint8_t *data,
                                 uint32_t len) {
-  if (len == DF_BLOCK && (reinterpret_cast<uintptr_t>(data) & 3) == 0)
-    return parse_block_dma<WRITE>(s, st, P, r_blk, data);
+  if (len % (PB_CH * 64) == 0 && len > 0 && (reinterpret_cast<uintptr_t>(data) & 3) == 0)
+    return parse_block_dma<WRITE>(s, st, P, r_blk, data, len);
   return parse_block_regs<WRITE>(s, P, r_blk, data, len);
 }
 
@@ -1041,6 +1048,9 @@ __device__ __forceinline__ uint32_t op_price(uint32_t f, float inv_total) {
   return (uint32_t)(c < 8 ? 8 : c > 120 ? 120 : c);
 }
 
+#ifndef ZT_PRICE_SAMPLE
+#define ZT_PRICE_SAMPLE 4
+#endif
 // greedy parse statistics -> prices (one wave per block, small LDS: many waves per CU)
 __global__ __launch_bounds__(64) void price_kernel(DeflateParams P) {
   __shared__ PriceShared sh;
@@ -1053,7 +1063,10 @@ __global__ __launch_bounds__(64) void price_kernel(DeflateParams P) {
   for (int i = lane; i < 288; i += 64) s->lit_hist[i] = 0;
   if (lane < 32) s->dist_hist[lane] = 0;
   wsync();
-  parse_block<false>(s, &s->stage, P, P.res + lo, P.base + P.halo + lo, blen);
+  // the prices only need symbol statistics: a greedy parse of the block's
+  // first 1/ZT_PRICE_SAMPLE (the full block when smaller) estimates them
+  const uint32_t plen = blen < (uint32_t)(DF_BLOCK / ZT_PRICE_SAMPLE) ? blen : (uint32_t)(DF_BLOCK / ZT_PRICE_SAMPLE);
+  parse_block<false>(s, &s->stage, P, P.res + lo, P.base + P.halo + lo, plen);
   wsync();
   BlockPrices *bp = reinterpret_cast<BlockPrices *>(P.slots + (size_t)blk * DF_SLOT);
   float tl = 0.f, td = 0.f;
