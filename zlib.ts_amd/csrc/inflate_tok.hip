@@ -156,9 +156,12 @@ __device__ __forceinline__ int tok_huffman(Reader &rd, const HuffTab *lt, const 
 // their true start until they merge with their old path (a marked position),
 // and the marks are corrected on the way.  A second pass decodes every lane's
 // exact range and writes its tokens at their final index.
-constexpr uint32_t SP_LANE_BITS = 960;                    // 120 bytes per lane
+#ifndef ZT_SP_LANE_BITS
+#define ZT_SP_LANE_BITS 480
+#endif
+constexpr uint32_t SP_LANE_BITS = ZT_SP_LANE_BITS;        // 60 bytes per lane: 18.5 KiB of LDS, 8 units per CU
 constexpr uint32_t SP_WORDS = SP_LANE_BITS / 32;          // bitmap words per lane
-constexpr uint32_t SP_STAGE_BYTES = 8192;                 // staged input per round
+constexpr uint32_t SP_STAGE_BYTES = IN_RING;              // staged input per round
 static_assert(64 * SP_LANE_BITS / 8 + 16 + 64 <= SP_STAGE_BYTES, "round must fit the stage");
 static_assert(SP_STAGE_BYTES <= 4 * IN_RING_WORDS, "stage lives in the reader's ring");
 
