@@ -1020,9 +1020,13 @@ constexpr int OP_SEG = 512;
 constexpr int OP_OV = 128;
 // C ring rows: C[i + l] for l <= OP_RING.  A longer match reads C[i + OP_RING]
 // instead of C[i + L] (an estimate of its continuation: the parse stays
-// valid, only the DP's cost model is approximate there); 132 rows keep the
-// LDS at 17 KiB per wave (9 waves per CU instead of 4 at 260 rows)
-constexpr int OP_RING = 132;
+// valid, only the DP's cost model is approximate there); 80 rows keep the
+// LDS at 11 KiB per wave (12 waves per CU, the VGPR limit, instead of 4 at
+// 260 rows); ratios unchanged to 4 digits on the bench corpora
+#ifndef ZT_OP_RING
+#define ZT_OP_RING 80
+#endif
+constexpr int OP_RING = ZT_OP_RING;
 constexpr int OP_SHORT = 16;
 constexpr int OP_PF = 4;      // groups of 16 positions prefetched per lane  // every cut length 3..OP_SHORT is tried, longer ones only at L
 
