@@ -153,6 +153,8 @@ __device__ __forceinline__ uint32_t ridx(uint32_t rel) { return rel & (DF_RING -
 __device__ __forceinline__ uint32_t ld8(const MatchShared *s, uint32_t rel) {
   return reinterpret_cast<const uint8_t *>(s->ring)[ridx(rel)];
 }
+// 4 bytes at any byte offset: two aligned dwords and a byte align (an
+// unaligned ds_read_b32 is legal on gfx950 but measured 25-45 % slower here)
 __device__ __forceinline__ uint32_t ld32(const MatchShared *s, uint32_t rel) {
   uint32_t i = ridx(rel);
   uint32_t w = i >> 2;
