@@ -48,28 +48,76 @@ bool inf_debug() {
 constexpr uint32_t kUnitTokCap = 32768 + 64;  // a 32 KiB block has <= 32768 tokens
 
 // sync point = byte after an aligned 00 00 FF FF; list entry = pos << 1 | restart
+// One 16-byte aligned chunk per lane, loaded as one 16-byte word; the 8 bytes
+// before it and the 12 after come from the neighbouring lanes (lanes at a
+// wave's edge load them).  A sync point is 00 00 FF FF (u32 0xFFFF0000 at the
+// candidate) ending at p; a restart point is the double marker
+// 00 00 00 FF FF 00 | 00 00 FF FF before it.
+__device__ __forceinline__ uint32_t fs_word(const uint8_t *in, uint64_t n, int64_t q) {
+  // 4 bytes at q (bytes outside [0, n) read as 1: never part of a pattern)
+  uint32_t v = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t x = q + k;
+    v |= (uint32_t)((x >= 0 && (uint64_t)x < n) ? in[x] : 1) << (8 * k);
+  }
+  return v;
+}
+constexpr uint32_t FS_ITER = 4;  // 4 KiB spans per workgroup (fewer, longer workgroups)
 __global__ __launch_bounds__(256) void find_syncs(const uint8_t *__restrict__ in, uint64_t lo, uint64_t n,
                                                   uint64_t *__restrict__ list, uint32_t *__restrict__ count) {
-  const uint64_t base = (lo & ~uint64_t(15)) + ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 16;
-  if (base >= n) return;
-  uint8_t b[26];
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const int lane = threadIdx.x & 63;
+  for (uint32_t it = 0; it < FS_ITER; ++it) {
+  const uint64_t base =
+      (lo & ~uint64_t(15)) + (((uint64_t)blockIdx.x * FS_ITER + it) * 256 + threadIdx.x) * 16;
+  // words: w[0..1] = bytes [base - 8, base), w[2..5] = [base, base + 16), w[6..8] = [base + 16, base + 28)
+  uint32_t w[9];
+  const bool whole = base + 16 <= n && (reinterpret_cast<uintptr_t>(in) & 15) == 0;
+  if (whole) {
+    const u32x4 v = *reinterpret_cast<const u32x4 *>(in + base);
+    w[2] = v.x;
+    w[3] = v.y;
+    w[4] = v.z;
+    w[5] = v.w;
+  } else {
 #pragma unroll
-  for (int j = 0; j < 26; ++j) {
-    const int64_t q = (int64_t)base - 6 + j;
-    b[j] = (q >= 0 && (uint64_t)q < n) ? in[q] : 1;
+    for (int k = 0; k < 4; ++k) w[2 + k] = fs_word(in, n, (int64_t)base + 4 * k);
   }
+  w[0] = (uint32_t)__shfl_up((int)w[4], 1, 64);
+  w[1] = (uint32_t)__shfl_up((int)w[5], 1, 64);
+  w[6] = (uint32_t)__shfl_down((int)w[2], 1, 64);
+  w[7] = (uint32_t)__shfl_down((int)w[3], 1, 64);
+  w[8] = (uint32_t)__shfl_down((int)w[4], 1, 64);
+  const bool aligned = (reinterpret_cast<uintptr_t>(in) & 3) == 0;
+  const uint32_t *in32 = reinterpret_cast<const uint32_t *>(in);
+  if (lane == 0) {
+    const bool ok = aligned && base >= 8 && base <= n;
+    w[0] = ok ? in32[(base - 8) / 4] : fs_word(in, n, (int64_t)base - 8);
+    w[1] = ok ? in32[(base - 4) / 4] : fs_word(in, n, (int64_t)base - 4);
+  }
+  if (lane == 63) {
+    const bool ok = aligned && base + 28 <= n;
+    w[6] = ok ? in32[(base + 16) / 4] : fs_word(in, n, (int64_t)base + 16);
+    w[7] = ok ? in32[(base + 20) / 4] : fs_word(in, n, (int64_t)base + 20);
+    w[8] = ok ? in32[(base + 24) / 4] : fs_word(in, n, (int64_t)base + 24);
+  }
+  if (base >= n) continue;
+  auto at = [&](int x) -> uint32_t {  // 4 bytes at base - 8 + x (0 <= x <= 32)
+    return (x & 3) ? __builtin_amdgcn_alignbyte(w[(x >> 2) + 1], w[x >> 2], x & 3) : w[x >> 2];
+  };
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
-    // bytes base + j .. base + j + 3 are b[j + 6 .. j + 9]
-    if (b[j + 6] == 0 && b[j + 7] == 0 && b[j + 8] == 0xFF && b[j + 9] == 0xFF) {
+    if (at(8 + j) == 0xFFFF0000u) {
       const uint64_t p = base + j + 4;
       if (p > lo && p < n) {
-        const bool restart = b[j] == 0 && b[j + 1] == 0 && b[j + 2] == 0 && b[j + 3] == 0xFF && b[j + 4] == 0xFF &&
-                             b[j + 5] == 0 && base + j >= 6;
+        // bytes base + j - 6 .. base + j - 1: 00 00 00 FF FF 00
+        const bool restart = base + j >= 6 && at(2 + j) == 0xFF000000u && (at(6 + j) & 0xFFFFu) == 0x00FFu;
         const uint32_t k = atomicAdd(count, 1u);
         if (k < kMaxSync) list[k] = (p << 1) | (restart ? 1 : 0);
       }
     }
+  }
   }
 }
 
@@ -87,7 +135,7 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   uint64_t *d_list = reinterpret_cast<uint64_t *>(static_cast<uint8_t *>(d_cand) + 256);
   ZT_HIP(hipMemsetAsync(d_count, 0, 4, s));
   const uint64_t span = n - (index & ~size_t(15));
-  const uint32_t grid = (uint32_t)((span + 16 * 256 - 1) / (16 * 256));
+  const uint32_t grid = (uint32_t)((span + 16 * 256 * FS_ITER - 1) / (16 * 256 * FS_ITER));
   ZT_TRY(timing_begin(c, s, 2));
   find_syncs<<<grid, 256, 0, s>>>(d_in, index, n, d_list, d_count);
   ZT_HIP(hipGetLastError());
