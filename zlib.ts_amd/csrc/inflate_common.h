@@ -12,8 +12,15 @@ namespace {
 constexpr int RING = 32768;
 constexpr uint32_t RING_MASK = RING - 1;
 constexpr int GRAN = 16384;  // output flush granule (ring holds 32 KiB of history)
-constexpr int PRI = 10;
+#ifndef ZT_PRI
+#define ZT_PRI 7
+#endif
+constexpr int PRI = ZT_PRI;
 
+// PRI: primary table bits.  7 (512 B per table) rather than 10: the decode
+// kernels' LDS shrinks enough for more units per CU, which outweighs the
+// canonical search of the rarer longer codes (tokenize 5.9 -> 5.1 ms per GiB;
+// measured 6..10).
 // Primary-table entry (u32): bits 0-3 code length (0 = code longer than PRI
 // bits: canonical search), 4-7 extra bits, 8-16 symbol, 17-31 base value
 // (match length for literal/length symbols > 256, distance for distance
