@@ -552,10 +552,13 @@ __global__ __launch_bounds__(DF_THREADS) void match_kernel(DeflateParams P) {
 }
 
 // ================================ 2. block_kernel ================================
+constexpr int PM_MAX = 2 * 286;  // package-merge list length bound (2m - 2)
 struct HufScratch {
-  uint32_t key[512];  // (freq << 9) | symbol, sorted ascending
-  uint32_t a[320];    // Moffat-Katajainen work array
-  uint32_t bl_count[40];
+  uint32_t key[320];              // (freq << 9) | symbol, sorted ascending (the first m are used)
+  uint32_t lst[2][PM_MAX];        // package-merge lists (weights), ping-pong
+  uint32_t pkg[14][PM_MAX / 32];  // per level: which list entries are packages
+  uint32_t items[16];             // selected items per level
+  uint32_t bl_count[16];
 };
 
 // parse staging ring (parse_block_dma)
@@ -643,7 +646,8 @@ __device__ __forceinline__ void sort_keys(HufScratch &h, const uint32_t *freq_in
   }
   reg_bitonic<R>(key, lane);
 #pragma unroll
-  for (int r = 0; r < R; ++r) h.key[lane * R + r] = key[r];
+  for (int r = 0; r < R; ++r)
+    if (lane * R + r < 320) h.key[lane * R + r] = key[r];
 }
 
 __device__ void huff_lengths(BlockShared *s, const uint32_t *freq_in, int n, int limit, uint8_t *len_out) {
@@ -678,97 +682,103 @@ __device__ void huff_lengths(BlockShared *s, const uint32_t *freq_in, int n, int
   else
     sort_keys<8>(h, freq_in, n, lane);
   wsync();
+  // Length-limited optimal code lengths by package-merge, wave-parallel: the
+  // level-j list is the items merged with the packages (pairs) of the level
+  // j-1 list, kept to its first 2m - 2 entries; each merge by merge-path
+  // (every lane a contiguous run of outputs after a binary search).  The
+  // selection is then a prefix of every level: c_L = 2m - 2 entries at the
+  // top, c_{j-1} = 2 x (packages among the first c_j), and item k's code
+  // length is the number of levels whose selected prefix holds it.
+  const uint32_t mm = m, cap = 2 * mm - 2;
+  for (uint32_t i = lane; i < mm; i += 64) h.lst[0][i] = h.key[i] >> 9;
+  for (int j = 0; j < limit - 1; ++j)
+    for (uint32_t w = lane; w < PM_MAX / 32; w += 64) h.pkg[j][w] = 0;
+  wsync();
+  uint32_t lp = mm;  // length of the previous level's list
+  for (int j = 1; j < limit; ++j) {
+    const uint32_t *P = h.lst[(j - 1) & 1];
+    uint32_t *Q = h.lst[j & 1];
+    const uint32_t np = lp / 2;
+    const uint32_t lq = mm + np < cap ? mm + np : cap;
+    auto A = [&](uint32_t i) -> uint32_t { return h.key[i] >> 9; };
+    auto B = [&](uint32_t i) -> uint32_t { return P[2 * i] + P[2 * i + 1]; };
+    const uint32_t per = (lq + 63) / 64;
+    const uint32_t d = (uint32_t)lane * per;
+    if (d < lq) {
+      // merge path: a = items among the first d outputs (items first on ties)
+      uint32_t lo = d > np ? d - np : 0, hi = d < mm ? d : mm;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (A(mid) <= B(d - mid - 1)) lo = mid + 1;
+        else hi = mid;
+      }
+      uint32_t ia = lo, ib = d - lo;
+      const uint32_t e = d + per < lq ? d + per : lq;
+      for (uint32_t o = d; o < e; ++o) {
+        const bool take_a = ib >= np || (ia < mm && A(ia) <= B(ib));
+        Q[o] = take_a ? A(ia) : B(ib);
+        if (!take_a) atomicOr(&h.pkg[j - 1][o >> 5], 1u << (o & 31));
+        ia += take_a ? 1 : 0;
+        ib += take_a ? 0 : 1;
+      }
+    }
+    wsync();
+    lp = lq;
+  }
+  // selection, top level down (lane 0; 15 steps of a popcount)
   if (lane == 0) {
-    uint32_t *A = h.a;
-    for (uint32_t i = 0; i < m; ++i) A[i] = h.key[i] >> 9;
-    // Moffat & Katajainen, in-place minimum-redundancy code lengths
-    int mm = (int)m;
-    int sidx = 0, r = 0;
-    for (int t = 0; t < mm - 1; ++t) {
-      if (sidx >= mm || (r < t && A[r] < A[sidx])) {
-        A[t] = A[r];
-        A[r] = t;
-        ++r;
-      } else {
-        A[t] = A[sidx];
-        ++sidx;
-      }
-      if (sidx >= mm || (r < t && A[r] < A[sidx])) {
-        A[t] += A[r];
-        A[r] = t;
-        ++r;
-      } else {
-        A[t] += A[sidx];
-        ++sidx;
-      }
+    uint32_t c = cap;
+    for (int j = limit - 1; j >= 1; --j) {
+      uint32_t pk = 0;
+      for (uint32_t w = 0; w < (c >> 5); ++w) pk += __popc(h.pkg[j - 1][w]);
+      if (c & 31) pk += __popc(h.pkg[j - 1][c >> 5] & ((1u << (c & 31)) - 1));
+      h.items[j] = c - pk;
+      c = 2 * pk;
     }
-    A[mm - 2] = 0;
-    for (int t = mm - 3; t >= 0; --t) A[t] = A[A[t]] + 1;
-    int avail = 1, used = 0, depth = 0, t = mm - 2, x = mm - 1;
-    while (avail > 0) {
-      while (t >= 0 && (int)A[t] == depth) {
-        ++used;
-        --t;
-      }
-      while (avail > used) {
-        A[x] = depth;
-        --x;
-        --avail;
-      }
-      avail = 2 * used;
-      ++depth;
-      used = 0;
-    }
-    // A[i] = length of the i-th least frequent symbol; limit via bl_count
-    uint32_t *bl = h.bl_count;
-    for (int i = 0; i < 40; ++i) bl[i] = 0;
-    int maxl = 0;
-    for (int i = 0; i < mm; ++i) {
-      int l = (int)A[i];
-      if (l > 39) l = 39;
-      bl[l]++;
-      if (l > maxl) maxl = l;
-    }
-    for (int i = maxl; i > limit; --i) {
-      while (bl[i] > 0) {
-        int j = i - 2;
-        while (bl[j] == 0) --j;
-        bl[i] -= 2;
-        bl[i - 1] += 1;
-        bl[j + 1] += 2;
-        bl[j] -= 1;
-      }
-    }
-    // longest codes go to the least frequent symbols
-    int l = limit < maxl ? limit : maxl;
-    int idx = 0;
-    for (; l >= 1; --l)
-      for (uint32_t c = 0; c < bl[l]; ++c) len_out[h.key[idx++] & 511] = (uint8_t)l;
+    h.items[0] = c;
+  }
+  wsync();
+  for (uint32_t k = lane; k < mm; k += 64) {
+    uint32_t l = 0;
+    for (int j = 0; j < limit; ++j) l += k < h.items[j] ? 1u : 0u;
+    len_out[h.key[k] & 511] = (uint8_t)l;
   }
   wsync();
 }
 
-// canonical codes (bit-reversed for LSB-first emission)
+// canonical codes (bit-reversed for LSB-first emission), wave-parallel: the
+// rank of a symbol among equal lengths by ballots per 64-symbol chunk
 __device__ void huff_codes(const uint8_t *len, int n, uint32_t *code) {
   const int lane = threadIdx.x & 63;
-  if (lane == 0) {
-    uint32_t cnt[16] = {0}, next[16];
-    for (int i = 0; i < n; ++i) cnt[len[i]]++;
-    cnt[0] = 0;
-    uint32_t c = 0;
-    for (int l = 1; l < 16; ++l) {
-      c = (c + cnt[l - 1]) << 1;
-      next[l] = c;
+  uint32_t cnt = 0;  // lane l < 16: symbols of length l
+  for (int b0 = 0; b0 < n; b0 += 64) {
+    const int i = b0 + lane;
+    const uint32_t l = i < n ? len[i] : 0u;
+#pragma unroll
+    for (int L = 1; L < 16; ++L) {
+      const uint32_t c = (uint32_t)__popcll(__ballot(l == (uint32_t)L));
+      if (lane == L) cnt += c;
     }
-    for (int i = 0; i < n; ++i) {
-      uint32_t l = len[i];
-      if (!l) {
-        code[i] = 0;
-        continue;
-      }
-      uint32_t v = next[l]++;
-      code[i] = (l << 16) | (__brev(v) >> (32 - l));
+  }
+  // first code of each length: next[l] = (next[l-1] + cnt[l-1]) << 1
+  uint32_t next = 0, run = 0;
+  for (int L = 1; L < 16; ++L) {
+    const uint32_t prev_cnt = L > 1 ? (uint32_t)__builtin_amdgcn_readlane((int)cnt, L - 1) : 0u;
+    run = (run + prev_cnt) << 1;
+    if (lane == L) next = run;
+  }
+  for (int b0 = 0; b0 < n; b0 += 64) {
+    const int i = b0 + lane;
+    const uint32_t l = i < n ? len[i] : 0u;
+    uint32_t v = 0;
+#pragma unroll
+    for (int L = 1; L < 16; ++L) {
+      const uint64_t peers = __ballot(l == (uint32_t)L);
+      const uint32_t base = (uint32_t)__builtin_amdgcn_readlane((int)next, L);
+      if (l == (uint32_t)L) v = base + (uint32_t)__popcll(peers & lanemask_lt(lane));
+      if (lane == L) next += (uint32_t)__popcll(peers);
     }
+    if (i < n) code[i] = l ? ((l << 16) | (__brev(v) >> (32 - l))) : 0u;
   }
   wsync();
 }
