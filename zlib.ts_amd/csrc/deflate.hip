@@ -871,8 +871,8 @@ __device__ __forceinline__ void parse_window(S *s, const DeflateParams &P, uint3
       const uint32_t step = L >= 3 ? L : 1;
       uint32_t ptr = i < len ? lane + step : 64u;
       uint64_t mask = i < len ? 1ull << lane : 0ull;
-#pragma unroll
-      for (int rnd = 0; rnd < 6; ++rnd) {
+      // rounds until every lane's chain has left the window (at most 6)
+      for (int rnd = 0; rnd < 6 && __ballot(ptr < 64); ++rnd) {
         const bool in = ptr < 64;
         const int src = in ? (int)ptr : lane;
         uint32_t mlo = __shfl((uint32_t)mask, src, 64);
