@@ -1281,57 +1281,111 @@ __global__ __launch_bounds__(64) void block_kernel(DeflateParams P) {
   huff_lengths(s, s->lit_hist, 286, 15, s->lit_len);
   huff_lengths(s, s->dist_hist, 30, 15, s->dist_len);
   BK_T(1);
-  if (lane == 0) {
-    uint32_t hlit = 286, hdist = 30;
-    while (hlit > 257 && s->lit_len[hlit - 1] == 0) --hlit;
-    while (hdist > 1 && s->dist_len[hdist - 1] == 0) --hdist;
-    s->hlit = hlit;
-    s->hdist = hdist;
-    // RLE of the concatenated lengths (RFC 1951 3.2.7)
-    uint32_t nsym = 0;
+  {
+    // trailing zero lengths trimmed (RFC 1951 3.2.7: HLIT >= 257, HDIST >= 1)
+    uint32_t hi_lit = 0;
+    for (int c = 0; c < 5; ++c) {
+      const int i = c * 64 + lane;
+      const uint64_t nz = __ballot(i < 286 && s->lit_len[i] != 0);
+      if (nz) hi_lit = (uint32_t)(c * 64 + 64 - __clzll(nz));
+    }
+    const uint64_t dnz = __ballot(lane < 30 && s->dist_len[lane] != 0);
+    const uint32_t hlit = hi_lit > 257 ? hi_lit : 257;
+    const uint32_t hdist = dnz ? (uint32_t)(64 - __clzll(dnz)) : 1u;
     const uint32_t total = hlit + hdist;
-    uint32_t clf[19] = {0};
-    uint32_t i = 0;
-    while (i < total) {
-      uint32_t v = i < hlit ? s->lit_len[i] : s->dist_len[i - hlit];
-      uint32_t run = 1;
-      while (i + run < total && (i + run < hlit ? s->lit_len[i + run] : s->dist_len[i + run - hlit]) == v) ++run;
-      i += run;
-      if (v == 0) {
-        while (run >= 11) {
-          uint32_t r = run < 138 ? run : 138;
-          s->cl_syms[nsym++] = 18 | ((r - 11) << 5);
-          clf[18]++;
-          run -= r;
+    if (lane < 19) s->cl_code[lane] = 0;  // CL symbol frequencies until the codes are built
+    if (lane == 0) {
+      s->hlit = hlit;
+      s->hdist = hdist;
+    }
+    wsync();
+    // RLE of the concatenated lengths, one lane per run: runs start where the
+    // value changes; each run's symbols are counted, placed by a scan, then
+    // written by its lane
+    auto val = [&](uint32_t i) -> uint32_t { return i < hlit ? s->lit_len[i] : s->dist_len[i - hlit]; };
+    uint64_t starts[5];
+    for (int c = 0; c < 5; ++c) {
+      const uint32_t i = (uint32_t)(c * 64 + lane);
+      starts[c] = __ballot(i < total && (i == 0 || val(i) != val(i - 1)));
+    }
+    uint32_t base = 0;
+    for (int c = 0; c < 5; ++c) {
+      const uint32_t i = (uint32_t)(c * 64 + lane);
+      const bool st = (starts[c] >> lane) & 1;
+      uint32_t v = 0, r = 0, cnt = 0;
+      if (st) {
+        // the run's end: the next start (or the end of the lengths)
+        uint32_t e = total;
+        const uint64_t rest = lane < 63 ? starts[c] & (~0ull << (lane + 1)) : 0ull;
+        if (rest) {
+          e = (uint32_t)(c * 64) + (uint32_t)__builtin_ctzll(rest);
+        } else {
+          for (int cc = c + 1; cc < 5; ++cc)
+            if (starts[cc]) {
+              e = (uint32_t)(cc * 64) + (uint32_t)__builtin_ctzll(starts[cc]);
+              break;
+            }
         }
-        if (run >= 3) {
-          s->cl_syms[nsym++] = 17 | ((run - 3) << 5);
-          clf[17]++;
-          run = 0;
+        v = val(i);
+        r = e - i;
+        // symbol count of the run (the writer below, counting only)
+        uint32_t q = r;
+        if (v == 0) {
+          while (q >= 11) {
+            q -= q < 138 ? q : 138;
+            ++cnt;
+          }
+          cnt += q >= 3 ? 1 : q;
+        } else {
+          cnt = 1;
+          --q;
+          while (q >= 3) {
+            q -= q < 6 ? q : 6;
+            ++cnt;
+          }
+          cnt += q;
         }
-        while (run--) {
-          s->cl_syms[nsym++] = 0;
-          clf[0]++;
-        }
-      } else {
-        s->cl_syms[nsym++] = v;
-        clf[v]++;
-        --run;
-        while (run >= 3) {
-          uint32_t r = run < 6 ? run : 6;
-          s->cl_syms[nsym++] = 16 | ((r - 3) << 5);
-          clf[16]++;
-          run -= r;
-        }
-        while (run--) {
-          s->cl_syms[nsym++] = v;
-          clf[v]++;
+      }
+      // exclusive scan of the counts
+      uint32_t incl = cnt;
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)incl, off, 64);
+        if (lane >= off) incl += y;
+      }
+      uint32_t o = base + incl - cnt;
+      base += (uint32_t)__shfl((int)incl, 63, 64);
+      if (st) {
+        uint32_t q = r;
+        if (v == 0) {
+          while (q >= 11) {
+            const uint32_t x = q < 138 ? q : 138;
+            s->cl_syms[o++] = (uint16_t)(18 | ((x - 11) << 5));
+            atomicAdd(&s->cl_code[18], 1u);
+            q -= x;
+          }
+          if (q >= 3) {
+            s->cl_syms[o++] = (uint16_t)(17 | ((q - 3) << 5));
+            atomicAdd(&s->cl_code[17], 1u);
+          } else if (q) {
+            atomicAdd(&s->cl_code[0], q);
+            for (; q; --q) s->cl_syms[o++] = 0;
+          }
+        } else {
+          s->cl_syms[o++] = (uint16_t)v;
+          uint32_t nv = 1;
+          --q;
+          while (q >= 3) {
+            const uint32_t x = q < 6 ? q : 6;
+            s->cl_syms[o++] = (uint16_t)(16 | ((x - 3) << 5));
+            atomicAdd(&s->cl_code[16], 1u);
+            q -= x;
+          }
+          for (; q; --q, ++nv) s->cl_syms[o++] = (uint16_t)v;
+          atomicAdd(&s->cl_code[v], nv);
         }
       }
     }
-    s->n_cl_syms = nsym;
-    // cl_code[] doubles as the CL symbol frequencies until the codes are built
-    for (int k = 0; k < 19; ++k) s->cl_code[k] = clf[k];
+    if (lane == 0) s->n_cl_syms = base;
   }
   wsync();
   BK_T(2);
