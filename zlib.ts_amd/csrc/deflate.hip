@@ -801,21 +801,6 @@ __device__ __forceinline__ uint32_t fixed_lit(uint32_t sym) {
   return (l << 16) | (__brev(c) >> (32 - l));
 }
 
-// serial bit writer for the header (lane 0): complete words go to the slot
-struct HdrOut {
-  uint32_t *slot;
-  uint64_t acc;
-  uint32_t nacc, word;
-  __device__ void put(uint32_t v, uint32_t n) {
-    acc |= (uint64_t)v << nacc;
-    nacc += n;
-    if (nacc >= 32) {
-      slot[word++] = (uint32_t)acc;
-      acc >>= 32;
-      nacc -= 32;
-    }
-  }
-};
 
 // LDS histogram increment as inline asm: the compiler puts an
 // s_waitcnt vmcnt(0) before every LDS store it sees while LDS-DMA loads are in
@@ -1437,33 +1422,59 @@ __global__ __launch_bounds__(64) void block_kernel(DeflateParams P) {
   for (int i = lane; i < 288; i += 64) plan->lit_code[i] = bt == 2 ? (i < 286 ? s->lit_code[i] : 0u) : fixed_lit(i);
   if (lane < 32) plan->dist_code[lane] = bt == 2 ? (lane < 30 ? s->dist_code[lane] : 0u)
                                                  : ((5u << 16) | (__brev((uint32_t)lane) >> 27));
-  if (lane == 0) {
-    HdrOut ho;
-    ho.slot = reinterpret_cast<uint32_t *>(P.slots + (size_t)blk * DF_SLOT);
-    ho.acc = 0;
-    ho.nacc = 0;
-    ho.word = 0;
-    if (bt == 1) {
-      ho.put(2, 3);  // BFINAL=0, BTYPE=01
-    } else if (bt == 2) {
-      ho.put(4, 3);  // BFINAL=0, BTYPE=10
-      ho.put(s->hlit - 257, 5);
-      ho.put(s->hdist - 1, 5);
-      ho.put(hclen - 4, 4);
-      for (uint32_t k = 0; k < hclen; ++k) ho.put(s->cl_len[kClOrder[k]], 3);
-      for (uint32_t k = 0; k < s->n_cl_syms; ++k) {
-        uint32_t cs = s->cl_syms[k], c = cs & 31;
-        uint32_t cc = s->cl_code[c];
-        ho.put(cc & 0xFFFF, cc >> 16);
-        if (c == 16) ho.put(cs >> 5, 2);
-        else if (c == 17) ho.put(cs >> 5, 3);
-        else if (c == 18) ho.put(cs >> 5, 7);
+  // the dynamic header, wave-parallel: every field an item (value, bits),
+  // bit offsets by a scan, OR-ed into an LDS word buffer (the package-merge
+  // list space, free now), complete words copied to the slot
+  uint32_t hbits = 0, htail = 0;
+  if (bt == 1) {
+    hbits = 3;
+    htail = 2;  // BFINAL=0, BTYPE=01
+  } else if (bt == 2) {
+    uint32_t *hw = s->huf.lst[0];
+    for (int k = lane; k < 160; k += 64) hw[k] = 0;
+    wsync();
+    const uint32_t nsym = s->n_cl_syms, nitems = 1 + hclen + nsym;
+    uint32_t base = 0;
+    for (uint32_t c0 = 0; c0 < nitems; c0 += 64) {
+      const uint32_t it = c0 + (uint32_t)lane;
+      uint32_t v = 0, nb = 0;
+      if (it == 0) {
+        v = 4u | ((s->hlit - 257) << 3) | ((s->hdist - 1) << 8) | ((hclen - 4) << 13);  // BTYPE=10, HLIT, HDIST, HCLEN
+        nb = 17;
+      } else if (it <= hclen) {
+        v = s->cl_len[kClOrder[it - 1]];
+        nb = 3;
+      } else if (it < nitems) {
+        const uint32_t cs = s->cl_syms[it - 1 - hclen], c = cs & 31;
+        const uint32_t cc = s->cl_code[c], cl = cc >> 16;
+        const uint32_t xb = c == 16 ? 2u : c == 17 ? 3u : c == 18 ? 7u : 0u;
+        v = (cc & 0xFFFF) | ((cs >> 5) << cl);
+        nb = cl + xb;
+      }
+      uint32_t incl = nb;
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)incl, off, 64);
+        if (lane >= off) incl += y;
+      }
+      const uint32_t o = base + incl - nb;
+      base += (uint32_t)__shfl((int)incl, 63, 64);
+      if (nb) {
+        const uint32_t sh = o & 31;
+        atomicOr(&hw[o >> 5], v << sh);
+        if (sh + nb > 32) atomicOr(&hw[(o >> 5) + 1], v >> (32 - sh));
       }
     }
+    wsync();
+    hbits = base;
+    uint32_t *slot = reinterpret_cast<uint32_t *>(P.slots + (size_t)blk * DF_SLOT);
+    for (uint32_t k = lane; k < (hbits >> 5); k += 64) slot[k] = hw[k];
+    htail = hw[hbits >> 5] & ((hbits & 31) ? ((1u << (hbits & 31)) - 1) : 0u);
+  }
+  if (lane == 0) {
     plan->ntok = ntok;
     plan->btype = bt;
-    plan->hdr_bits = ho.word * 32 + ho.nacc;
-    plan->hdr_tail = (uint32_t)ho.acc;
+    plan->hdr_bits = hbits;
+    plan->hdr_tail = htail;
     plan->blen = blen;
     plan->last = last ? 1 : 0;
   }
