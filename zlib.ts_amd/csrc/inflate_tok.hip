@@ -862,7 +862,12 @@ __global__ __launch_bounds__(64) void copy_kernel(ResolveParams P) {
       const uint64_t upto = flushed + RS_FLUSH;
       cp_flush(&sh, out, flushed, upto, lane);
       flushed = upto;
+#ifdef ZT_CP_FLUSH_WAIT
       __builtin_amdgcn_s_waitcnt(0x0F70);  // keep vmcnt counting descriptor chunks only
+#endif
+      // (no wait here: vector memory operations retire in issue order, so the
+      // counted descriptor waits above only wait longer with the stores in
+      // flight, never shorter)
     }
   }
   wave_sync();
