@@ -78,6 +78,7 @@ __global__ __launch_bounds__(CK_THREADS) void checksum_segments(const uint8_t *_
                                                                  size_t hi, size_t nseg,
                                                                  const uint32_t *__restrict__ nib_g,
                                                                  const uint32_t *__restrict__ x2n_g,
+                                                                 const uint32_t *__restrict__ shift_g,
                                                                  SegResult *__restrict__ out) {
   // 32 KiB of replicated nibble tables + the combine scratch
   __shared__ uint32_t T[DO_CRC ? NIB_ENTRIES * 32 : 1];
@@ -85,6 +86,7 @@ __global__ __launch_bounds__(CK_THREADS) void checksum_segments(const uint8_t *_
   __shared__ uint32_t red_c[CK_THREADS];
   __shared__ uint32_t red_l[CK_THREADS];
   __shared__ unsigned long long red_a[CK_THREADS / 64][2];
+  __shared__ uint32_t red_w[CK_THREADS / 64];
 
   const int tid = threadIdx.x;
   const int lane32 = tid & 31;
@@ -149,8 +151,22 @@ __global__ __launch_bounds__(CK_THREADS) void checksum_segments(const uint8_t *_
         red_a[tid >> 6][1] = a2;
       }
     }
+    // a segment of whole slices merges with fixed shifts: slice t's CRC
+    // moves over the (255 - t) KiB after it (one multiplication), then XOR
+    const bool whole = seg_lo >= lo && seg_lo + CK_SEG <= hi;
+    if (DO_CRC && whole) {
+      uint32_t x = multmodp(shift_g[tid], c);
+      for (int off = 32; off > 0; off >>= 1) x ^= (uint32_t)__shfl_xor((int)x, off, 64);
+      if ((tid & 63) == 0) red_w[tid >> 6] = x;
+    }
     __syncthreads();
-    if (DO_CRC) {
+    if (DO_CRC && whole) {
+      if (tid == 0) {
+        uint32_t x = 0;
+        for (int w = 0; w < CK_THREADS / 64; ++w) x ^= red_w[w];
+        red_c[0] = x;
+      }
+    } else if (DO_CRC) {
 #pragma unroll 1
       for (int step = 1; step < CK_THREADS; step <<= 1) {
         if ((tid & (2 * step - 1)) == 0) {
@@ -164,76 +180,108 @@ __global__ __launch_bounds__(CK_THREADS) void checksum_segments(const uint8_t *_
         __syncthreads();
       }
     }
-    if (tid == 0) {
-      SegResult r;
-      r.crc = DO_CRC ? red_c[0] : 0;
-      uint64_t t1 = 0, t2 = 0;
-      if (DO_ADLER) {
-        for (int w = 0; w < CK_THREADS / 64; ++w) {
-          t1 += red_a[w][0];
-          t2 += red_a[w][1];
+    if (tid < 64) {
+      // move the segment over the bytes that follow it in the buffer so the
+      // finish is a plain XOR / sum: x^(8 * after) as the product of the
+      // base-64 digit factors, one per lane 0..7, by a 3-level butterfly
+      const size_t sv_lo = seg_lo > lo ? seg_lo : lo;
+      const size_t sv_hi = (seg_lo + CK_SEG) < hi ? (seg_lo + CK_SEG) : hi;
+      const uint64_t after = hi - sv_hi;
+      uint32_t f = 1u << 31;  // x^0
+      if (DO_CRC) {
+        if (tid < ZT_CRC_DIGITS) {
+          const uint32_t v = (uint32_t)(after >> (6 * tid)) & 63u;
+          if (v) f = shift_g[ZT_CRC_DIG_OFF + tid * 64 + v];
         }
+        for (int o = 1; o < 8; o <<= 1) f = multmodp(f, (uint32_t)__shfl_xor((int)f, o, 64));
       }
-      r.s1 = (uint32_t)(t1 % 65521u);
-      r.s2 = (uint32_t)(t2 % 65521u);
-      size_t sv_lo = seg_lo > lo ? seg_lo : lo;
-      size_t sv_hi = (seg_lo + CK_SEG) < hi ? (seg_lo + CK_SEG) : hi;
-      r.len = sv_hi > sv_lo ? (uint32_t)(sv_hi - sv_lo) : 0;
-      out[seg] = r;
+      if (tid == 0) {
+        SegResult r;
+        r.crc = 0;
+        if (DO_CRC) {
+          uint32_t x = multmodp(f, red_c[0]);
+          const uint64_t rest = after >> (6 * ZT_CRC_DIGITS);
+          if (rest) x = multmodp(x2nmodp(x2n, rest, 3 + 6 * ZT_CRC_DIGITS), x);
+          r.crc = x;
+        }
+        uint64_t t1 = 0, t2 = 0;
+        if (DO_ADLER) {
+          for (int w = 0; w < CK_THREADS / 64; ++w) {
+            t1 += red_a[w][0];
+            t2 += red_a[w][1];
+          }
+        }
+        r.s1 = (uint32_t)(t1 % 65521u);
+        r.s2 = (uint32_t)((t2 % 65521u + (after % 65521u) * r.s1) % 65521u);
+        r.len = sv_hi > sv_lo ? (uint32_t)(sv_hi - sv_lo) : 0;
+        out[seg] = r;
+      }
     }
     __syncthreads();
   }
 }
 
-// Merge per-segment results in order and apply the callers' initial values.
-__global__ __launch_bounds__(256) void checksum_finish(const SegResult *__restrict__ segs, size_t nseg, uint64_t n,
-                                                       const uint32_t *__restrict__ x2n_g, uint32_t crc_in,
-                                                       uint32_t adler_in, uint32_t *__restrict__ result) {
-  __shared__ uint32_t x2n[32];
-  __shared__ uint32_t rc[256];
-  __shared__ uint64_t rl[256];
-  __shared__ uint64_t r1[256], r2[256];
-  const int tid = threadIdx.x;
-  if (tid < 32) x2n[tid] = x2n_g[tid];
-  __syncthreads();
-  // thread t folds a contiguous run of segments
-  const size_t per = (nseg + 255) / 256;
-  const size_t b = (size_t)tid * per, e = (b + per) < nseg ? (b + per) : nseg;
+// x^(8 n) * c mod P from the base-64 digit tables (ZT_CRC_DIGITS digits;
+// longer shifts finish with the squares table)
+__device__ inline uint32_t shift_bytes(const uint32_t *__restrict__ dig, const uint32_t *__restrict__ x2n,
+                                       uint64_t n, uint32_t c) {
+#pragma unroll
+  for (int d = 0; d < ZT_CRC_DIGITS; ++d) {
+    const uint32_t v = (uint32_t)(n >> (6 * d)) & 63u;
+    if (v) c = multmodp(dig[d * 64 + v], c);
+  }
+  const uint64_t rest = n >> (6 * ZT_CRC_DIGITS);
+  if (rest) c = multmodp(x2nmodp(x2n, rest, 3 + 6 * ZT_CRC_DIGITS), c);
+  return c;
+}
+
+// Merge per-segment results (already moved to the end of the buffer by
+// checksum_segments) and apply the callers' initial values.
+#define CF_THREADS 1024
+__global__ __launch_bounds__(CF_THREADS) void checksum_finish(const SegResult *__restrict__ segs, size_t nseg,
+                                                              size_t hi, uint64_t n,
+                                                              const uint32_t *__restrict__ x2n_g,
+                                                              const uint32_t *__restrict__ shift_g, uint32_t crc_in,
+                                                              uint32_t adler_in, uint32_t *__restrict__ result) {
+  __shared__ uint32_t red_c[CF_THREADS / 64];
+  __shared__ uint64_t red_1[CF_THREADS / 64], red_2[CF_THREADS / 64];
+  const uint32_t *dig = shift_g + ZT_CRC_DIG_OFF;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   uint32_t c = 0;
-  uint64_t l = 0, s1 = 0, s2 = 0;
-  for (size_t i = b; i < e; ++i) {
-    SegResult r = segs[i];
-    if (r.len) c = multmodp(x2nmodp(x2n, r.len, 3), c);
+  uint64_t t1 = 0, t2 = 0;
+  for (size_t i = tid; i < nseg; i += CF_THREADS) {
+    const SegResult r = segs[i];
     c ^= r.crc;
-    s2 = (s2 + (uint64_t)r.len % 65521u * s1 + r.s2) % 65521u;
-    s1 = (s1 + r.s1) % 65521u;
-    l += r.len;
+    t1 += r.s1;
+    t2 += r.s2;
   }
-  rc[tid] = c;
-  rl[tid] = l;
-  r1[tid] = s1;
-  r2[tid] = s2;
+  for (int o = 32; o; o >>= 1) {
+    c ^= __shfl_xor(c, o);
+    t1 += __shfl_xor(t1, o);
+    t2 += __shfl_xor(t2, o);
+  }
+  if (lane == 0) {
+    red_c[wv] = c;
+    red_1[wv] = t1;
+    red_2[wv] = t2;
+  }
   __syncthreads();
-  for (int step = 1; step < 256; step <<= 1) {
-    if ((tid & (2 * step - 1)) == 0) {
-      uint64_t L = rl[tid + step];
-      if (L) rc[tid] = multmodp(x2nmodp(x2n, L, 3), rc[tid]);
-      rc[tid] ^= rc[tid + step];
-      r2[tid] = (r2[tid] + L % 65521u * r1[tid] + r2[tid + step]) % 65521u;
-      r1[tid] = (r1[tid] + r1[tid + step]) % 65521u;
-      rl[tid] += L;
-    }
-    __syncthreads();
-  }
   if (tid == 0) {
+    uint32_t raw = 0;
+    uint64_t r1 = 0, r2 = 0;
+    for (int w = 0; w < CF_THREADS / 64; ++w) {
+      raw ^= red_c[w];
+      r1 += red_1[w];
+      r2 += red_2[w];
+    }
+    r1 %= 65521u;
+    r2 %= 65521u;
     // CRC32.update: ~(shift(~crc, n) ^ raw)
-    uint32_t pre = ~crc_in;
-    pre = multmodp(x2nmodp(x2n, n, 3), pre);
-    result[0] = ~(pre ^ rc[0]);
+    result[0] = ~(shift_bytes(dig, x2n_g, n, ~crc_in) ^ raw);
     // Adler32.update: s1 = adler & 0xFFFF, s2 = (adler >> 16) & 0xFFFF (need not be reduced)
     uint64_t a = adler_in & 0xFFFFu, bb = (adler_in >> 16) & 0xFFFFu;
-    uint64_t f1 = (a + r1[0]) % 65521u;
-    uint64_t f2 = (bb + (n % 65521u) * (a % 65521u) + r2[0]) % 65521u;
+    uint64_t f1 = (a + r1) % 65521u;
+    uint64_t f2 = (bb + (n % 65521u) * (a % 65521u) + r2) % 65521u;
     result[1] = (uint32_t)((f2 << 16) | f1);
   }
 }
@@ -261,6 +309,14 @@ void crc_host_tables(uint32_t byte_table[256], uint32_t nib[256], uint32_t x2n[3
   for (int k = 1; k < 32; ++k) x2n[k] = multmodp(x2n[k - 1], x2n[k - 1]);
 }
 
+void crc_shift_tables(const uint32_t x2n[32], uint32_t shift[ZT_CRC_SHIFT_N]) {
+  for (int t = 0; t < CK_THREADS; ++t) shift[t] = x2nmodp(x2n, (uint64_t)CK_SLICE * (CK_THREADS - 1 - t), 3);
+  shift[CK_THREADS] = x2nmodp(x2n, CK_SEG, 3);
+  // digit tables: x^(8 * v * 64^d)
+  for (int d = 0; d < ZT_CRC_DIGITS; ++d)
+    for (uint64_t v = 0; v < 64; ++v) shift[ZT_CRC_DIG_OFF + d * 64 + v] = x2nmodp(x2n, v << (6 * d), 3);
+}
+
 int checksums_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, bool do_crc, bool do_adler, uint32_t crc_in,
                   uint32_t adler_in, uint32_t *d_result, hipStream_t s) {
   const uintptr_t addr = reinterpret_cast<uintptr_t>(d_in);
@@ -272,13 +328,16 @@ int checksums_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, bool do_crc, bool
   SegResult *segs = static_cast<SegResult *>(segbuf);
   const int grid = (int)(nseg < (size_t)c->num_cu * 8 ? nseg : (size_t)c->num_cu * 8);
   if (do_crc && do_adler)
-    checksum_segments<true, true><<<grid, CK_THREADS, 0, s>>>(frame, lo, hi, nseg, c->d_crc_nib, c->d_crc_x2n, segs);
+    checksum_segments<true, true><<<grid, CK_THREADS, 0, s>>>(frame, lo, hi, nseg, c->d_crc_nib, c->d_crc_x2n,
+                                                              c->d_crc_shift, segs);
   else if (do_crc)
-    checksum_segments<true, false><<<grid, CK_THREADS, 0, s>>>(frame, lo, hi, nseg, c->d_crc_nib, c->d_crc_x2n, segs);
+    checksum_segments<true, false><<<grid, CK_THREADS, 0, s>>>(frame, lo, hi, nseg, c->d_crc_nib, c->d_crc_x2n,
+                                                               c->d_crc_shift, segs);
   else
-    checksum_segments<false, true><<<grid, CK_THREADS, 0, s>>>(frame, lo, hi, nseg, c->d_crc_nib, c->d_crc_x2n, segs);
+    checksum_segments<false, true><<<grid, CK_THREADS, 0, s>>>(frame, lo, hi, nseg, c->d_crc_nib, c->d_crc_x2n,
+                                                               c->d_crc_shift, segs);
   ZT_HIP(hipGetLastError());
-  checksum_finish<<<1, 256, 0, s>>>(segs, nseg, n, c->d_crc_x2n, crc_in, adler_in, d_result);
+  checksum_finish<<<1, CF_THREADS, 0, s>>>(segs, nseg, hi, n, c->d_crc_x2n, c->d_crc_shift, crc_in, adler_in, d_result);
   ZT_HIP(hipGetLastError());
   return ZT_OK;
 }

@@ -73,6 +73,10 @@ int get_ctx(DeviceCtx **out) {
     ZT_HIP(hipMalloc(&c->d_crc_x2n, sizeof x2n));
     ZT_HIP(hipMemcpy(c->d_crc_nib, nib, sizeof nib, hipMemcpyHostToDevice));
     ZT_HIP(hipMemcpy(c->d_crc_x2n, x2n, sizeof x2n, hipMemcpyHostToDevice));
+    uint32_t shift[ZT_CRC_SHIFT_N] = {};
+    crc_shift_tables(x2n, shift);
+    ZT_HIP(hipMalloc(&c->d_crc_shift, sizeof shift));
+    ZT_HIP(hipMemcpy(c->d_crc_shift, shift, sizeof shift, hipMemcpyHostToDevice));
     for (auto &e : c->ev) ZT_HIP(hipEventCreate(&e));
     g_ctx[g_dev] = c;
   }

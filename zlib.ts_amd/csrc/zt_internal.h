@@ -36,6 +36,7 @@ struct DeviceCtx {
   // checksum constants (uploaded once)
   uint32_t *d_crc_nib = nullptr;    // 16 x 16 nibble tables (slice-by-8)
   uint32_t *d_crc_x2n = nullptr;    // x^(2^k) mod P, k = 0..31
+  uint32_t *d_crc_shift = nullptr;  // checksum.hip merge constants (crc_shift_tables)
   // scratch
   void *d_buf[8] = {};
   size_t buf_size[8] = {};
@@ -109,6 +110,12 @@ typedef __attribute__((address_space(1))) const uint8_t g_u8;
 typedef __attribute__((address_space(1))) const uint32_t g_u32;
 
 void crc_host_tables(uint32_t byte_table[256], uint32_t nib[256], uint32_t x2n[32]);
+// x^(8 L) mod P for the checksum kernels: [0, 256] fixed slice/segment merge
+// shifts, then ZT_CRC_DIGITS tables of 64 entries x^(8 v 64^d)
+#define ZT_CRC_DIGITS 6
+#define ZT_CRC_DIG_OFF 264
+#define ZT_CRC_SHIFT_N (ZT_CRC_DIG_OFF + 64 * ZT_CRC_DIGITS)
+void crc_shift_tables(const uint32_t x2n[32], uint32_t shift[ZT_CRC_SHIFT_N]);
 
 // ---- launchers (device-resident) ------------------------------------------------
 int checksums_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, bool do_crc, bool do_adler, uint32_t crc_in,
