@@ -157,6 +157,37 @@ def test_batch(zt, oracle):
     assert res[-1][0] == -12  # unknown BTYPE: 3
 
 
+def test_batch_two_phase_matches_one_wave(zt, oracle):
+    """Batches of >= 8 non-strict streams decode two-phase (tokenize + expand +
+    copy per stream); each stream's status, output and end ip must equal the
+    one-wave decode of the same stream alone (a batch of one), including
+    truncated, bit-flipped and trailing-garbage streams."""
+    rng = random.Random(11)
+    streams = []
+    for i in range(48):
+        n = rng.choice([1, 100, 5000, 65536, 150000])
+        d = oracle.gen(["xorshift32", "wordsalad", "structured"][i % 3], 700 + i, n)
+        s = zlib.compress(d, rng.choice([1, 6, 9]))[2:-4]
+        kind = i % 4
+        if kind == 1 and len(s) > 4:
+            s = s[: rng.randrange(1, len(s))]  # truncated
+        elif kind == 2 and len(s) > 4:
+            b = bytearray(s)
+            for _ in range(3):
+                q = rng.randrange(len(b))
+                b[q] ^= 1 << rng.randrange(8)
+            s = bytes(b)  # corrupted
+        elif kind == 3:
+            s = s + bytes(rng.randrange(256) for _ in range(17))  # trailing bytes
+        streams.append(s)
+    got = zt.inflate_raw_batch(streams)
+    for s, g in zip(streams, got):
+        (w,) = zt.inflate_raw_batch([s])
+        assert g[0] == w[0]
+        if w[0] == 0:
+            assert g[1] == w[1] and g[2] == w[2]
+
+
 def test_errors(zt):
     import ztamd
 

@@ -1,4 +1,5 @@
 // inflate_api.cpp -- host side of the inflate entry points (include/zt.h).
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -32,6 +33,142 @@ int inflate_error(int status, int detail) {
 
 static size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
+// Two-phase batch decode (inflate_tok.hip applied per stream): one tokenize
+// wave per stream (no history ring in LDS, so many streams per CU), then
+// expand + copy with one segment per stream, all outputs in one buffer.
+// Streams it cannot finish (errors, a token overflow, an empty input) are
+// appended to `failed` for the one-wave decoder, which also yields the
+// reference's exact error. Outputs of the others are malloc'd and filled.
+static int batch_two_phase(DeviceCtx *c, const uint8_t *d_in, const std::vector<size_t> &in_off, const size_t *n,
+                           const size_t *index, size_t count, uint8_t **out, size_t *out_len,
+                           std::vector<InfResult> &res, std::vector<size_t> &failed) {
+  hipStream_t s = c->stream;
+  std::vector<size_t> ids;
+  for (size_t i = 0; i < count; ++i) {
+    const size_t st = index ? index[i] : 0;
+    if (n[i] > st)
+      ids.push_back(i);
+    else
+      failed.push_back(i);
+  }
+  if (ids.empty()) return ZT_OK;
+  const size_t units = ids.size();
+  std::vector<TokJob> jobs(units);
+  uint64_t tok_total = 0;
+  for (size_t k = 0; k < units; ++k) {
+    const size_t i = ids[k];
+    TokJob &j = jobs[k];
+    j.start = in_off[i] + (index ? index[i] : 0);
+    j.end = in_off[i] + n[i];
+    // tokens <= output bytes; every token takes >= 1 input bit
+    uint64_t cap = std::max<uint64_t>(65536, 4 * (uint64_t)n[i]);
+    cap = std::min<uint64_t>(cap, (j.end - j.start) * 8) + 64;
+    cap = std::min<uint64_t>(cap, 1u << 30);
+    j.tok_off = tok_total;
+    j.tok_cap = (uint32_t)cap;
+    j.stop_first = 0;
+    tok_total += align_up(cap, 64);
+  }
+  void *d_tok, *d_meta;
+  ZT_TRY(scratch(c, 4, (tok_total + 256) * 4, &d_tok));  // + slack: chunked token reads
+  const size_t jobs_bytes = align_up(units * sizeof(TokJob), 256);
+  ZT_TRY(scratch(c, 6, jobs_bytes + align_up(units * sizeof(TokResult), 256), &d_meta));
+  TokJob *d_jobs = static_cast<TokJob *>(d_meta);
+  TokResult *d_tres = reinterpret_cast<TokResult *>(static_cast<uint8_t *>(d_meta) + jobs_bytes);
+  ZT_HIP(hipMemcpyAsync(d_jobs, jobs.data(), units * sizeof(TokJob), hipMemcpyHostToDevice, s));
+  TokParams tp{};
+  tp.in = d_in;
+  tp.n = 0;
+  tp.stops = reinterpret_cast<const uint64_t *>(d_meta);  // never read: nstops = 0
+  tp.nstops = 0;
+  tp.jobs = d_jobs;
+  tp.res = d_tres;
+  tp.tokens = static_cast<uint32_t *>(d_tok);
+  tp.count = (uint32_t)units;
+  tp.simt = 1;
+  tp.dbg = nullptr;
+  tp.dump_unit = 0xFFFFFFFFu;
+  tp.dump_once = 0;
+  ZT_TRY(tokenize_units_dev(tp, s));
+  std::vector<TokResult> tr(units);
+  ZT_HIP(hipMemcpyAsync(tr.data(), d_tres, units * sizeof(TokResult), hipMemcpyDeviceToHost, s));
+  ZT_HIP(hipStreamSynchronize(s));
+  // one chain unit and one segment per stream that decoded to BFINAL
+  std::vector<ChainUnit> chain;
+  std::vector<SegJob> segs;
+  std::vector<size_t> who;
+  uint64_t out_total = 0, desc_total = 0;
+  for (size_t k = 0; k < units; ++k) {
+    const TokResult &r = tr[k];
+    if (r.status != ZT_OK || r.stop_idx >= 0 || r.out_len > 0xFFFFFFFFull) {
+      failed.push_back(ids[k]);
+      continue;
+    }
+    desc_total = align_up(desc_total, 512);
+    segs.push_back(SegJob{(uint32_t)chain.size(), 1});
+    chain.push_back(ChainUnit{jobs[k].tok_off, out_total, out_total, desc_total, r.ntok, (uint32_t)r.out_len});
+    who.push_back(k);
+    out_total += align_up(r.out_len ? r.out_len : 1, 256);
+    desc_total += r.out_len;
+  }
+  if (chain.empty()) return ZT_OK;
+  void *d_out, *d_chain, *d_desc;
+  ZT_TRY(scratch(c, 1, out_total, &d_out));
+  const size_t chain_bytes = align_up(chain.size() * sizeof(ChainUnit), 256);
+  const size_t seg_bytes = align_up(segs.size() * sizeof(SegJob), 256);
+  const size_t ust_bytes = align_up(chain.size() * 4, 256);
+  ZT_TRY(scratch(c, 7, chain_bytes + seg_bytes + 2 * ust_bytes, &d_chain));
+  ZT_TRY(scratch(c, 3, (desc_total + 1024) * 2, &d_desc));  // + slack: chunked descriptor reads
+  ChainUnit *d_cu = static_cast<ChainUnit *>(d_chain);
+  SegJob *d_sj = reinterpret_cast<SegJob *>(static_cast<uint8_t *>(d_chain) + chain_bytes);
+  int32_t *d_ust = reinterpret_cast<int32_t *>(static_cast<uint8_t *>(d_chain) + chain_bytes + seg_bytes);
+  int32_t *d_st = reinterpret_cast<int32_t *>(static_cast<uint8_t *>(d_chain) + chain_bytes + seg_bytes + ust_bytes);
+  ZT_HIP(hipMemcpyAsync(d_cu, chain.data(), chain.size() * sizeof(ChainUnit), hipMemcpyHostToDevice, s));
+  ZT_HIP(hipMemcpyAsync(d_sj, segs.data(), segs.size() * sizeof(SegJob), hipMemcpyHostToDevice, s));
+  ResolveParams rp;
+  rp.tokens = static_cast<const uint32_t *>(d_tok);
+  rp.units = d_cu;
+  rp.segs = d_sj;
+  rp.out = static_cast<uint8_t *>(d_out);
+  rp.desc = static_cast<uint16_t *>(d_desc);
+  rp.unit_status = d_ust;
+  rp.seg_status = d_st;
+  rp.nunits = (uint32_t)chain.size();
+  rp.nseg = (uint32_t)segs.size();
+  ZT_TRY(resolve_segments_dev(rp, s));
+  std::vector<int32_t> ust(chain.size()), sst(segs.size());
+  ZT_HIP(hipMemcpyAsync(ust.data(), d_ust, chain.size() * 4, hipMemcpyDeviceToHost, s));
+  ZT_HIP(hipMemcpyAsync(sst.data(), d_st, segs.size() * 4, hipMemcpyDeviceToHost, s));
+  void *h;
+  ZT_TRY(pinned(c, out_total, &h));
+  ZT_HIP(hipMemcpyAsync(h, d_out, out_total, hipMemcpyDeviceToHost, s));
+  ZT_HIP(hipStreamSynchronize(s));
+  const uint8_t *stage = static_cast<const uint8_t *>(h);
+  std::vector<size_t> done;
+  for (size_t j = 0; j < chain.size(); ++j) {
+    const size_t k = who[j], i = ids[k];
+    if (ust[j] != ZT_OK || sst[j] != ZT_OK) {
+      failed.push_back(i);
+      continue;
+    }
+    out[i] = (uint8_t *)malloc(chain[j].out_len ? chain[j].out_len : 1);
+    if (!out[i]) return set_error(ZT_E_NOMEM, "host allocation failed");
+    out_len[i] = chain[j].out_len;
+    InfResult &r = res[i];
+    r = InfResult{};
+    r.out_len = chain[j].out_len;
+    r.end_ip = ((tr[k].end_bits + 7) >> 3) - in_off[i];
+    r.status = ZT_OK;
+    r.stop_idx = -1;
+    done.push_back(j);
+  }
+  parallel_copy(done.size(), [&](size_t q) {
+    const size_t j = done[q], i = ids[who[j]];
+    if (chain[j].out_len) memcpy(out[i], stage + chain[j].out_off, chain[j].out_len);
+  }, out_total);
+  return ZT_OK;
+}
+
 // Decode `count` host streams; outputs are malloc'd.
 static int inflate_host_batch(const uint8_t *const *in, const size_t *n, const size_t *index, size_t count,
                               const zt_inflate_opts *opts, uint8_t **out, size_t *out_len, size_t *end_ip,
@@ -52,12 +189,27 @@ static int inflate_host_batch(const uint8_t *const *in, const size_t *n, const s
   ZT_TRY(scratch(c, 0, in_total, &d_in));
   ZT_TRY(scratch(c, 2, count * (sizeof(InfJob) + sizeof(InfResult)) + 256, &d_jobs));
   d_res = (uint8_t *)d_jobs + align_up(count * sizeof(InfJob), 256);
-  for (size_t i = 0; i < count; ++i)
-    if (n[i]) ZT_HIP(hipMemcpyAsync((uint8_t *)d_in + in_off[i], in[i], n[i], hipMemcpyHostToDevice, c->stream));
+  // inputs packed into pinned staging, one H2D copy
+  {
+    void *h;
+    ZT_TRY(pinned(c, in_total, &h));
+    uint8_t *stage = (uint8_t *)h;
+    parallel_copy(count, [&](size_t i) { if (n[i]) memcpy(stage + in_off[i], in[i], n[i]); }, in_total);
+    ZT_HIP(hipMemcpyAsync(d_in, stage, in_total, hipMemcpyHostToDevice, c->stream));
+  }
   std::vector<InfJob> jobs(count);
   std::vector<InfResult> res(count);
-  std::vector<size_t> todo(count);
-  for (size_t i = 0; i < count; ++i) todo[i] = i;
+  std::vector<size_t> todo;
+  // non-strict batches of several streams: two-phase first, one wave per
+  // stream for whatever it leaves (ZT_BATCH_ONEWAVE=1 forces the latter)
+  static const bool onewave = getenv("ZT_BATCH_ONEWAVE") != nullptr;
+  if (!strict && count >= 8 && !onewave) {
+    ZT_TRY(batch_two_phase(c, (const uint8_t *)d_in, in_off, n, index, count, out, out_len, res, todo));
+    std::sort(todo.begin(), todo.end());
+  } else {
+    todo.resize(count);
+    for (size_t i = 0; i < count; ++i) todo[i] = i;
+  }
   for (int pass = 0; pass < 2 && !todo.empty(); ++pass) {
     size_t out_total = 0;
     std::vector<size_t> out_off(todo.size());
@@ -82,7 +234,10 @@ static int inflate_host_batch(const uint8_t *const *in, const size_t *n, const s
     std::vector<InfResult> r(todo.size());
     ZT_HIP(hipMemcpyAsync(r.data(), d_res, todo.size() * sizeof(InfResult), hipMemcpyDeviceToHost, c->stream));
     ZT_HIP(hipStreamSynchronize(c->stream));
-    std::vector<size_t> again;
+    std::vector<size_t> again, done;
+    // finished outputs are packed on the device side already (out_off);
+    // one D2H of the span up to the last finished byte into pinned staging
+    size_t span = 0;
     for (size_t k = 0; k < todo.size(); ++k) {
       size_t i = todo[k];
       res[i] = r[k];
@@ -96,13 +251,22 @@ static int inflate_host_batch(const uint8_t *const *in, const size_t *n, const s
       if (r[k].status == ZT_OK) {
         out[i] = (uint8_t *)malloc(r[k].out_len ? r[k].out_len : 1);
         if (!out[i]) return set_error(ZT_E_NOMEM, "host allocation failed");
-        if (r[k].out_len)
-          ZT_HIP(hipMemcpyAsync(out[i], (uint8_t *)d_out + out_off[k], r[k].out_len, hipMemcpyDeviceToHost,
-                                c->stream));
         out_len[i] = r[k].out_len;
+        done.push_back(k);
+        if (out_off[k] + r[k].out_len > span) span = out_off[k] + r[k].out_len;
       }
     }
-    ZT_HIP(hipStreamSynchronize(c->stream));
+    if (span) {
+      void *h;
+      ZT_TRY(pinned(c, span, &h));
+      const uint8_t *stage = (const uint8_t *)h;
+      ZT_HIP(hipMemcpyAsync(h, d_out, span, hipMemcpyDeviceToHost, c->stream));
+      ZT_HIP(hipStreamSynchronize(c->stream));
+      parallel_copy(done.size(), [&](size_t j) {
+        const size_t k = done[j], i = todo[k];
+        if (out_len[i]) memcpy(out[i], stage + out_off[k], out_len[i]);
+      }, span);
+    }
     todo.swap(again);
   }
   int first = ZT_OK;

@@ -167,6 +167,7 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
     const uint64_t left = n - j.start;
     j.tok_cap = (uint32_t)std::min<uint64_t>(kUnitTokCap, left * 8 + 64);
     j.stop_first = (uint32_t)i;  // sync[i] is the first sync point after start
+    j.end = 0;
   }
   void *d_tok, *d_meta;
   ZT_TRY(scratch(c, 4, (units * (size_t)kUnitTokCap + 256) * 4, &d_tok));  // + slack: chunked token reads

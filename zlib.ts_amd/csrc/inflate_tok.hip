@@ -488,7 +488,7 @@ __global__ __launch_bounds__(64) void tokenize_kernel(TokParams P) {
   const uint32_t u = blockIdx.x;
   const int lane = threadIdx.x & 63;
   const TokJob job = P.jobs[u];
-  const uint64_t n = P.n;
+  const uint64_t n = job.end ? job.end : P.n;
   Reader rd;
   rd.init(P.in, n, job.start, sh.inbuf, lane);
   TokOut to;

@@ -2,6 +2,8 @@
 //
 // Every entry point computes on the GPU.  There is deliberately no CPU
 // fallback: without a HIP device the calls fail with ZT_E_NO_DEVICE.
+#include <functional>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -99,6 +101,40 @@ int scratch(DeviceCtx *c, int slot, size_t bytes, void **ptr) {
   }
   *ptr = c->d_buf[slot];
   return ZT_OK;
+}
+
+int pinned(DeviceCtx *c, size_t bytes, void **ptr) {
+  if (bytes == 0) bytes = 16;
+  if (c->pinned_size < bytes) {
+    if (c->h_pinned) {
+      ZT_HIP(hipStreamSynchronize(c->stream));
+      ZT_HIP(hipHostFree(c->h_pinned));
+      c->h_pinned = nullptr;
+      c->pinned_size = 0;
+    }
+    size_t sz = bytes + bytes / 4;
+    ZT_HIP(hipHostMalloc(&c->h_pinned, sz, hipHostMallocDefault));
+    c->pinned_size = sz;
+  }
+  *ptr = c->h_pinned;
+  return ZT_OK;
+}
+
+void parallel_copy(size_t count, const std::function<void(size_t)> &fn, size_t total_bytes) {
+  // host memcpy fan-out for the batch paths: one thread per ~8 MiB, at most 8
+  size_t nt = total_bytes >> 23;
+  if (nt > 8) nt = 8;
+  if (nt > count) nt = count;
+  if (nt < 2) {
+    for (size_t i = 0; i < count; ++i) fn(i);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (size_t t = 0; t < nt; ++t)
+    th.emplace_back([&, t] {
+      for (size_t i = t; i < count; i += nt) fn(i);
+    });
+  for (auto &x : th) x.join();
 }
 
 }  // namespace zt

@@ -1,5 +1,6 @@
 // zt_internal.h -- shared host/device helpers for libzt (not installed).
 #pragma once
+#include <functional>
 #include <hip/hip_runtime.h>
 
 #include <cstddef>
@@ -58,6 +59,10 @@ int timing_collect(DeviceCtx *c, double *acc_ms, uint64_t *count, int k = 0);
 int get_ctx(DeviceCtx **out);
 // Grow-only device scratch slot `slot` to at least `bytes`.
 int scratch(DeviceCtx *c, int slot, size_t bytes, void **ptr);
+// Grow-only pinned host staging buffer (one per context) of at least `bytes`.
+int pinned(DeviceCtx *c, size_t bytes, void **ptr);
+// fn(0 .. count-1) over a few host threads when total_bytes is large.
+void parallel_copy(size_t count, const std::function<void(size_t)> &fn, size_t total_bytes);
 
 // ---- CRC-32 algebra (reflected, P = 0xEDB88320) ------------------------------
 // Host and device copies of zlib-style polynomial arithmetic: shifting a raw
@@ -157,6 +162,7 @@ struct TokJob {
   uint64_t tok_off;     // first token slot
   uint32_t tok_cap;     // token capacity
   uint32_t stop_first;  // index of the first sync point after `start`
+  uint64_t end;         // end of the unit's input (batch: its stream's end), 0: TokParams::n
 };
 struct TokResult {
   uint64_t out_len;   // bytes the unit's tokens produce
