@@ -1834,9 +1834,16 @@ static size_t deflate_geometry(const DeviceCtx *c, size_t n, DeflateGeom *g) {
   return g->res_bytes + g->slot_bytes + g->len_bytes + g->off_bytes + g->plan_bytes + 256;
 }
 
+// tuning hook: ZT_DF_RESTART = blocks per independent segment (>= 8, rounded
+// up to a multiple of the blocks per workgroup)
+static uint32_t restart_blocks() {
+  static const int e = getenv("ZT_DF_RESTART") ? atoi(getenv("ZT_DF_RESTART")) : 0;
+  return e >= 8 ? (uint32_t)e : kRestartBlocks;
+}
+
 size_t deflate_bound_bytes(size_t n) {
   size_t nb = (n + DF_BLOCK - 1) / DF_BLOCK;
-  return n + nb * 16 + (nb / kRestartBlocks + 1) * kRestartMarkerLen + 64;
+  return n + nb * 16 + (nb / 8 + 1) * kRestartMarkerLen + 64;
 }
 
 int deflate_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t halo, int final_, int ctype, int level,
@@ -1871,7 +1878,7 @@ int deflate_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t halo, in
   P.end = halo + n;
   P.blocks_per_wg = G.k;
   P.nblocks = G.nblocks;
-  P.restart = kRestartBlocks;
+  P.restart = (restart_blocks() + G.k - 1) / G.k * G.k;
   P.final_ = final_;
   const DeflateLevel L = level_params(level);
   P.max_chain = L.max_chain;
