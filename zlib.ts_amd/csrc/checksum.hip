@@ -73,6 +73,20 @@ __device__ __forceinline__ void adler16(uint32_t &s1, uint32_t &s2, uint4 v) {
   s1 += s;
 }
 
+// x^(8 n) * c mod P from the base-64 digit tables (ZT_CRC_DIGITS digits;
+// longer shifts finish with the squares table)
+__device__ inline uint32_t shift_bytes(const uint32_t *__restrict__ dig, const uint32_t *__restrict__ x2n,
+                                       uint64_t n, uint32_t c) {
+#pragma unroll
+  for (int d = 0; d < ZT_CRC_DIGITS; ++d) {
+    const uint32_t v = (uint32_t)(n >> (6 * d)) & 63u;
+    if (v) c = multmodp(dig[d * 64 + v], c);
+  }
+  const uint64_t rest = n >> (6 * ZT_CRC_DIGITS);
+  if (rest) c = multmodp(x2nmodp(x2n, rest, 3 + 6 * ZT_CRC_DIGITS), c);
+  return c;
+}
+
 template <bool DO_CRC, bool DO_ADLER>
 __global__ __launch_bounds__(CK_THREADS) void checksum_segments(const uint8_t *__restrict__ frame, size_t lo,
                                                                  size_t hi, size_t nseg,
@@ -83,15 +97,20 @@ __global__ __launch_bounds__(CK_THREADS) void checksum_segments(const uint8_t *_
   // 32 KiB of replicated nibble tables + the combine scratch
   __shared__ uint32_t T[DO_CRC ? NIB_ENTRIES * 32 : 1];
   __shared__ uint32_t x2n[32];
-  __shared__ uint32_t red_c[CK_THREADS];
-  __shared__ uint32_t red_l[CK_THREADS];
+  __shared__ uint32_t red_c[1];
   __shared__ unsigned long long red_a[CK_THREADS / 64][2];
   __shared__ uint32_t red_w[CK_THREADS / 64];
 
   const int tid = threadIdx.x;
   const int lane32 = tid & 31;
   if (DO_CRC) {
-    for (int i = tid; i < NIB_ENTRIES * 32; i += CK_THREADS) T[i] = nib_g[i >> 5];
+    // all loads in flight before the LDS stores (one call's latency matters
+    // for small inputs)
+    uint32_t tv[NIB_ENTRIES * 32 / CK_THREADS];
+#pragma unroll
+    for (int k = 0; k < NIB_ENTRIES * 32 / CK_THREADS; ++k) tv[k] = nib_g[(tid + k * CK_THREADS) >> 5];
+#pragma unroll
+    for (int k = 0; k < NIB_ENTRIES * 32 / CK_THREADS; ++k) T[tid + k * CK_THREADS] = tv[k];
     if (tid < 32) x2n[tid] = x2n_g[tid];
   }
   __syncthreads();
@@ -122,20 +141,28 @@ __global__ __launch_bounds__(CK_THREADS) void checksum_segments(const uint8_t *_
     } else if (v_lo < v_hi) {
       // ragged slice (first/last segment only): byte at a time
       len = (uint32_t)(v_hi - v_lo);
-      for (size_t i = v_lo; i < v_hi; ++i) {
-        uint32_t b = frame[i];
-        if (DO_CRC) c = crc_byte(c, b);
-        if (DO_ADLER) {
-          s1 += b;
+      size_t i = v_lo;
+      if (DO_CRC) {
+        // 8 bytes per step through the nibble tables, the rest a byte at a time
+        for (; i + 8 <= v_hi; i += 8) {
+          uint32_t w0 = 0, w1 = 0;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            w0 |= (uint32_t)frame[i + k] << (8 * k);
+            w1 |= (uint32_t)frame[i + 4 + k] << (8 * k);
+          }
+          c = crc_step8(c, w0, w1, T, lane32);
+        }
+        for (; i < v_hi; ++i) c = crc_byte(c, frame[i]);
+      }
+      if (DO_ADLER) {
+        for (size_t j = v_lo; j < v_hi; ++j) {
+          s1 += frame[j];
           s2 += s1;
         }
       }
     }
     // ---- merge slices inside the segment ----
-    if (DO_CRC) {
-      red_c[tid] = c;
-      red_l[tid] = len;
-    }
     uint64_t a1 = s1, a2 = 0;
     if (DO_ADLER) {
       // bytes after this slice within the segment's valid range
@@ -151,35 +178,29 @@ __global__ __launch_bounds__(CK_THREADS) void checksum_segments(const uint8_t *_
         red_a[tid >> 6][1] = a2;
       }
     }
-    // a segment of whole slices merges with fixed shifts: slice t's CRC
-    // moves over the (255 - t) KiB after it (one multiplication), then XOR
+    // slice t's CRC moves over the bytes after it inside the segment (one
+    // multiplication by the fixed x^(8 (255 - t) KiB) for a segment of whole
+    // slices, digit-table shifts otherwise), then XOR
     const bool whole = seg_lo >= lo && seg_lo + CK_SEG <= hi;
-    if (DO_CRC && whole) {
-      uint32_t x = multmodp(shift_g[tid], c);
+    if (DO_CRC) {
+      uint32_t x;
+      if (whole) {
+        x = multmodp(shift_g[tid], c);
+      } else {
+        const size_t seg_v_hi = (seg_lo + CK_SEG) < hi ? (seg_lo + CK_SEG) : hi;
+        const uint64_t after = (len && seg_v_hi > v_hi) ? seg_v_hi - v_hi : 0;
+        x = len ? shift_bytes(shift_g + ZT_CRC_DIG_OFF, x2n, after, c) : 0u;
+      }
       for (int off = 32; off > 0; off >>= 1) x ^= (uint32_t)__shfl_xor((int)x, off, 64);
       if ((tid & 63) == 0) red_w[tid >> 6] = x;
     }
     __syncthreads();
-    if (DO_CRC && whole) {
-      if (tid == 0) {
-        uint32_t x = 0;
-        for (int w = 0; w < CK_THREADS / 64; ++w) x ^= red_w[w];
-        red_c[0] = x;
-      }
-    } else if (DO_CRC) {
-#pragma unroll 1
-      for (int step = 1; step < CK_THREADS; step <<= 1) {
-        if ((tid & (2 * step - 1)) == 0) {
-          uint32_t rl = red_l[tid + step];
-          uint32_t rc = red_c[tid + step];
-          uint32_t lc = red_c[tid];
-          if (rl) lc = multmodp(x2nmodp(x2n, rl, 3), lc);
-          red_c[tid] = lc ^ rc;
-          red_l[tid] += rl;
-        }
-        __syncthreads();
-      }
+    if (DO_CRC && tid == 0) {
+      uint32_t x = 0;
+      for (int w = 0; w < CK_THREADS / 64; ++w) x ^= red_w[w];
+      red_c[0] = x;
     }
+    __syncthreads();
     if (tid < 64) {
       // move the segment over the bytes that follow it in the buffer so the
       // finish is a plain XOR / sum: x^(8 * after) as the product of the
@@ -219,20 +240,6 @@ __global__ __launch_bounds__(CK_THREADS) void checksum_segments(const uint8_t *_
     }
     __syncthreads();
   }
-}
-
-// x^(8 n) * c mod P from the base-64 digit tables (ZT_CRC_DIGITS digits;
-// longer shifts finish with the squares table)
-__device__ inline uint32_t shift_bytes(const uint32_t *__restrict__ dig, const uint32_t *__restrict__ x2n,
-                                       uint64_t n, uint32_t c) {
-#pragma unroll
-  for (int d = 0; d < ZT_CRC_DIGITS; ++d) {
-    const uint32_t v = (uint32_t)(n >> (6 * d)) & 63u;
-    if (v) c = multmodp(dig[d * 64 + v], c);
-  }
-  const uint64_t rest = n >> (6 * ZT_CRC_DIGITS);
-  if (rest) c = multmodp(x2nmodp(x2n, rest, 3 + 6 * ZT_CRC_DIGITS), c);
-  return c;
 }
 
 // Merge per-segment results (already moved to the end of the buffer by
