@@ -331,7 +331,7 @@ int checksums_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, bool do_crc, bool
   const size_t lo = addr & 15, hi = lo + n;
   const size_t nseg = n ? (hi + CK_SEG - 1) / CK_SEG : 1;
   void *segbuf;
-  ZT_TRY(scratch(c, 3, nseg * sizeof(SegResult), &segbuf));
+  ZT_TRY(scratch(c, 8, nseg * sizeof(SegResult), &segbuf));
   SegResult *segs = static_cast<SegResult *>(segbuf);
   const int grid = (int)(nseg < (size_t)c->num_cu * 8 ? nseg : (size_t)c->num_cu * 8);
   if (do_crc && do_adler)

@@ -53,19 +53,28 @@ int deflate_with_checksums(const uint8_t *in, size_t n, const zt_deflate_opts *o
   ZT_TRY(scratch(c, 3, ss, &d_scr));
   ZT_TRY(scratch(c, 2, 16, &d_res));
   if (n) ZT_HIP(hipMemcpyAsync(d_in, in, n, hipMemcpyHostToDevice, c->stream));
+  // the checksums run on the second stream beside the deflate pipeline (both
+  // only read the input); every return below waits for that stream first
+  uint32_t sums[2] = {0, 1};  // CRC-32 and Adler-32 of nothing
+  struct AuxWait {
+    hipStream_t s;
+    ~AuxWait() { (void)hipStreamSynchronize(s); }
+  } aux_wait{c->aux};
+  if (n) {
+    ZT_HIP(hipEventRecord(c->aux_ev, c->stream));
+    ZT_HIP(hipStreamWaitEvent(c->aux, c->aux_ev, 0));
+    ZT_TRY(checksums_dev(c, (const uint8_t *)d_in, n, crc != nullptr, adler != nullptr, 0, 1, (uint32_t *)d_res,
+                         c->aux));
+    ZT_HIP(hipMemcpyAsync(sums, d_res, sizeof sums, hipMemcpyDeviceToHost, c->aux));
+  }
   size_t len = 0;
   ZT_TRY(deflate_dev_run(c, (const uint8_t *)d_in, n, 0, 1, ct, lv, (uint8_t *)d_out, &len, d_scr, ss, c->stream));
-  uint32_t sums[2] = {0, 1};  // CRC-32 and Adler-32 of nothing
-  if (n) {
-    ZT_TRY(checksums_dev(c, (const uint8_t *)d_in, n, crc != nullptr, adler != nullptr, 0, 1, (uint32_t *)d_res,
-                         c->stream));
-    ZT_HIP(hipMemcpyAsync(sums, d_res, sizeof sums, hipMemcpyDeviceToHost, c->stream));
-  }
   uint8_t *h = (uint8_t *)malloc(prefix_len + len + trailer + 1);
   if (!h) return set_error(ZT_E_NOMEM, "host allocation failed");
   if (prefix_len) memcpy(h, prefix, prefix_len);
   if (len) ZT_HIP(hipMemcpyAsync(h + prefix_len, d_out, len, hipMemcpyDeviceToHost, c->stream));
-  const hipError_t e = hipStreamSynchronize(c->stream);
+  hipError_t e = hipStreamSynchronize(c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->aux);
   if (e != hipSuccess) {
     free(h);
     return hip_fail(e, "hipStreamSynchronize");

@@ -490,7 +490,7 @@ __global__ __launch_bounds__(DF_THREADS) void match_kernel(DeflateParams P) {
   for (uint32_t p0 = 0; p0 < re; p0 += DF_SUB) {
     const uint32_t p1 = (p0 + DF_SUB) < re ? (p0 + DF_SUB) : re;
     lds_barrier();
-    uint64_t t0, t1, t2, t3;
+    [[maybe_unused]] uint64_t t0, t1, t2, t3;
     DF_T(t0);
     uint32_t ih = p1 >= kext ? p1 - kext : 0;
     if (rend >= kext && ih > rend - kext) ih = rend - kext;

@@ -296,9 +296,9 @@ __device__ __forceinline__ void inflate_stream(const InfJob &job, InfResult &res
       }
       wr.op = uni64(wr.op);
       int clen;
-      uint64_t t0 = PROF_T();
+      [[maybe_unused]] uint64_t t0 = PROF_T();
       int sym = decode_sym<STRICT>(rd, lt, clen);
-      uint64_t t1 = PROF_T();
+      [[maybe_unused]] uint64_t t1 = PROF_T();
       PROF_ADD(0, t1 - t0);
       PROF_ADD(8, 1);
       if (sym < 0) {
@@ -346,7 +346,7 @@ __device__ __forceinline__ void inflate_stream(const InfJob &job, InfResult &res
         break;
       }
       // parallel copy: byte i comes from history[src + (i mod dist)]
-      uint64_t t2 = PROF_T();
+      [[maybe_unused]] uint64_t t2 = PROF_T();
       PROF_ADD(2, t2 - t1);
       PROF_ADD(9, 1);
       PROF_ADD(10, length);
@@ -391,8 +391,8 @@ __global__ __launch_bounds__(64) void inflate_batch_kernel(const InfJob *__restr
   if (j >= count) return;
   InfJob job = jobs[j];
   InfResult res;
-  const uint64_t t0 = PROF_T();
-  const int lane = threadIdx.x & 63;
+  [[maybe_unused]] const uint64_t t0 = PROF_T();
+  [[maybe_unused]] const int lane = threadIdx.x & 63;
   if (job.strict)
     inflate_stream<true>(job, res, &sh);
   else

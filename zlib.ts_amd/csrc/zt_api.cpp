@@ -66,6 +66,8 @@ int get_ctx(DeviceCtx **out) {
     DeviceCtx *c = new DeviceCtx();
     c->device = g_dev;
     ZT_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    ZT_HIP(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+    ZT_HIP(hipEventCreateWithFlags(&c->aux_ev, hipEventDisableTiming));
     hipDeviceProp_t prop;
     ZT_HIP(hipGetDeviceProperties(&prop, g_dev));
     c->num_cu = prop.multiProcessorCount;
@@ -90,7 +92,7 @@ int scratch(DeviceCtx *c, int slot, size_t bytes, void **ptr) {
   if (bytes == 0) bytes = 16;
   if (c->buf_size[slot] < bytes) {
     if (c->d_buf[slot]) {
-      ZT_HIP(hipStreamSynchronize(c->stream));
+      ZT_HIP(hipDeviceSynchronize());  // any stream may still use it
       ZT_HIP(hipFree(c->d_buf[slot]));
       c->d_buf[slot] = nullptr;
       c->buf_size[slot] = 0;
@@ -107,7 +109,7 @@ int pinned(DeviceCtx *c, size_t bytes, void **ptr) {
   if (bytes == 0) bytes = 16;
   if (c->pinned_size < bytes) {
     if (c->h_pinned) {
-      ZT_HIP(hipStreamSynchronize(c->stream));
+      ZT_HIP(hipDeviceSynchronize());
       ZT_HIP(hipHostFree(c->h_pinned));
       c->h_pinned = nullptr;
       c->pinned_size = 0;

@@ -39,8 +39,11 @@ struct DeviceCtx {
   uint32_t *d_crc_x2n = nullptr;    // x^(2^k) mod P, k = 0..31
   uint32_t *d_crc_shift = nullptr;  // checksum.hip merge constants (crc_shift_tables)
   // scratch
-  void *d_buf[8] = {};
-  size_t buf_size[8] = {};
+  void *d_buf[10] = {};  // slot 8: checksum segment partials
+  size_t buf_size[10] = {};
+  // second stream: checksums run beside the deflate pipeline in the containers
+  hipStream_t aux = nullptr;
+  hipEvent_t aux_ev = nullptr;
   void *h_pinned = nullptr;
   // zt_timing_enable: HIP-event kernel timing
   bool timing = false;
