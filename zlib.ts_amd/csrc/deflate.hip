@@ -1807,9 +1807,11 @@ static DeflateLevel level_params(int level) {
   }
 }
 
-// Work split: enough workgroups to cover every CU twice, at most 8 blocks
-// (256 KiB) per workgroup (small super-chunks balance uneven data across
-// CUs; each loads 28 KiB of history), a power of two so segments (32 blocks) align.
+// Work split: enough workgroups to cover every CU twice, at most 4 blocks
+// (128 KiB) per workgroup (small super-chunks balance uneven data across
+// CUs; each loads 28 KiB of history; 1 GiB mixed corpus, match kernel:
+// 8 / 4 / 2 blocks 31.8 / 30.7 / 31.4 ms), a power of two so segments (32
+// blocks) align.
 struct DeflateGeom {
   uint32_t nblocks, k, nwg;
   size_t res_bytes, slot_bytes, len_bytes, off_bytes, plan_bytes;
@@ -1821,7 +1823,7 @@ static size_t deflate_geometry(const DeviceCtx *c, size_t n, DeflateGeom *g) {
   uint32_t kk = (g->nblocks + 2 * c->num_cu - 1) / (2 * c->num_cu);
   // tuning hook: ZT_DF_SUPER caps the blocks per workgroup (power of two <= 32)
   static const int cap_env = getenv("ZT_DF_SUPER") ? atoi(getenv("ZT_DF_SUPER")) : 0;
-  const uint32_t cap = cap_env > 0 && cap_env <= 32 ? (uint32_t)cap_env : 8u;
+  const uint32_t cap = cap_env > 0 && cap_env <= 32 ? (uint32_t)cap_env : 4u;
   uint32_t k2 = 1;
   while (k2 < kk && k2 < cap) k2 <<= 1;
   g->k = k2;
