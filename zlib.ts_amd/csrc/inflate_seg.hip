@@ -123,6 +123,20 @@ __global__ __launch_bounds__(256) void find_syncs(const uint8_t *__restrict__ in
 
 size_t align256(size_t v) { return (v + 255) & ~size_t(255); }
 
+// LSD radix sort (11-bit digits) of the sync-point list, up to `max_key`:
+// the atomic-append order of find_syncs is only roughly ascending, and a
+// comparison sort of ~32 K entries per GiB costs about 1 ms of host time
+void radix_sort(std::vector<uint64_t> &v, uint64_t max_key) {
+  std::vector<uint64_t> tmp(v.size());
+  for (int sh = 0; sh < 64 && (max_key >> sh); sh += 11) {
+    uint32_t cnt[2049] = {};
+    for (uint64_t e : v) ++cnt[((e >> sh) & 2047) + 1];
+    for (int i = 0; i < 2048; ++i) cnt[i + 1] += cnt[i];
+    for (uint64_t e : v) tmp[cnt[(e >> sh) & 2047]++] = e;
+    v.swap(tmp);
+  }
+}
+
 }  // namespace
 
 int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t index, uint8_t **d_out_io,
@@ -146,7 +160,7 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   std::vector<uint64_t> raw(cnt);
   ZT_HIP(hipMemcpyAsync(raw.data(), d_list, (size_t)cnt * 8, hipMemcpyDeviceToHost, s));
   ZT_HIP(hipStreamSynchronize(s));
-  std::sort(raw.begin(), raw.end());
+  radix_sort(raw, (uint64_t)n << 1 | 1);
   std::vector<uint64_t> sync;
   std::vector<uint8_t> restart;
   sync.reserve(raw.size());
