@@ -25,6 +25,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "zt_internal.h"
@@ -157,9 +158,19 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   ZT_HIP(hipMemcpyAsync(&cnt, d_count, 4, hipMemcpyDeviceToHost, s));
   ZT_HIP(hipStreamSynchronize(s));
   if (cnt == 0 || cnt > kMaxSync) FALLBACK("%u sync points\n", cnt);
-  std::vector<uint64_t> raw(cnt);
-  ZT_HIP(hipMemcpyAsync(raw.data(), d_list, (size_t)cnt * 8, hipMemcpyDeviceToHost, s));
+  // metadata moves through pinned staging (slot 1):
+  // [list | jobs | results | chain | segments | statuses]
+  void *hp;
+  const size_t units_max = (size_t)cnt + 1;
+  const size_t meta_a = align256((size_t)cnt * 8) + align256(units_max * sizeof(TokJob)) +
+                        align256(units_max * sizeof(TokResult));
+  const size_t meta_b = align256(units_max * sizeof(ChainUnit)) + align256(units_max * sizeof(SegJob)) +
+                        2 * align256(units_max * 4);
+  ZT_TRY(pinned(c, meta_a + meta_b, &hp, 1));
+  uint8_t *pin = static_cast<uint8_t *>(hp);
+  ZT_HIP(hipMemcpyAsync(pin, d_list, (size_t)cnt * 8, hipMemcpyDeviceToHost, s));
   ZT_HIP(hipStreamSynchronize(s));
+  std::vector<uint64_t> raw(reinterpret_cast<uint64_t *>(pin), reinterpret_cast<uint64_t *>(pin) + cnt);
   radix_sort(raw, (uint64_t)n << 1 | 1);
   std::vector<uint64_t> sync;
   std::vector<uint8_t> restart;
@@ -193,7 +204,9 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   TokJob *d_jobs = reinterpret_cast<TokJob *>(static_cast<uint8_t *>(d_meta) + stops_bytes);
   TokResult *d_res = reinterpret_cast<TokResult *>(static_cast<uint8_t *>(d_meta) + stops_bytes + jobs_bytes);
   ZT_HIP(hipMemcpyAsync(d_stops, sync.data(), sync.size() * 8, hipMemcpyHostToDevice, s));
-  ZT_HIP(hipMemcpyAsync(d_jobs, jobs.data(), units * sizeof(TokJob), hipMemcpyHostToDevice, s));
+  TokJob *h_jobs = reinterpret_cast<TokJob *>(pin + align256((size_t)cnt * 8));
+  memcpy(h_jobs, jobs.data(), units * sizeof(TokJob));
+  ZT_HIP(hipMemcpyAsync(d_jobs, h_jobs, units * sizeof(TokJob), hipMemcpyHostToDevice, s));
   TokParams tp;
   tp.in = d_in;
   tp.n = n;
@@ -218,8 +231,8 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   ZT_TRY(timing_begin(c, s, 3));
   ZT_TRY(tokenize_units_dev(tp, s));
   ZT_TRY(timing_end(c, s, 3));
-  std::vector<TokResult> res(units);
-  ZT_HIP(hipMemcpyAsync(res.data(), d_res, units * sizeof(TokResult), hipMemcpyDeviceToHost, s));
+  TokResult *res = reinterpret_cast<TokResult *>(pin + align256((size_t)cnt * 8) + align256(units_max * sizeof(TokJob)));
+  ZT_HIP(hipMemcpyAsync(res, d_res, units * sizeof(TokResult), hipMemcpyDeviceToHost, s));
   ZT_HIP(hipStreamSynchronize(s));
   if (check) {
     std::vector<uint64_t> dbg(units * 8);
@@ -298,8 +311,15 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   SegJob *d_sj = reinterpret_cast<SegJob *>(static_cast<uint8_t *>(d_chain) + chain_bytes);
   int32_t *d_ust = reinterpret_cast<int32_t *>(static_cast<uint8_t *>(d_chain) + chain_bytes + seg_bytes);
   int32_t *d_st = reinterpret_cast<int32_t *>(static_cast<uint8_t *>(d_chain) + chain_bytes + seg_bytes + ust_bytes);
-  ZT_HIP(hipMemcpyAsync(d_cu, chain.data(), chain.size() * sizeof(ChainUnit), hipMemcpyHostToDevice, s));
-  ZT_HIP(hipMemcpyAsync(d_sj, segs.data(), segs.size() * sizeof(SegJob), hipMemcpyHostToDevice, s));
+  ChainUnit *h_cu = reinterpret_cast<ChainUnit *>(pin + meta_a);
+  SegJob *h_sj = reinterpret_cast<SegJob *>(pin + meta_a + align256(units_max * sizeof(ChainUnit)));
+  int32_t *h_ust = reinterpret_cast<int32_t *>(pin + meta_a + align256(units_max * sizeof(ChainUnit)) +
+                                               align256(units_max * sizeof(SegJob)));
+  int32_t *h_st = h_ust + align256(units_max * 4) / 4;
+  memcpy(h_cu, chain.data(), chain.size() * sizeof(ChainUnit));
+  memcpy(h_sj, segs.data(), segs.size() * sizeof(SegJob));
+  ZT_HIP(hipMemcpyAsync(d_cu, h_cu, chain.size() * sizeof(ChainUnit), hipMemcpyHostToDevice, s));
+  ZT_HIP(hipMemcpyAsync(d_sj, h_sj, segs.size() * sizeof(SegJob), hipMemcpyHostToDevice, s));
   ResolveParams rp;
   rp.tokens = static_cast<const uint32_t *>(d_tok);
   rp.units = d_cu;
@@ -312,17 +332,15 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   rp.nseg = (uint32_t)segs.size();
   ZT_TRY(resolve_segments_dev(rp, s));
   ZT_TRY(timing_end(c, s, 2));
-  std::vector<int32_t> ust(chain.size());
-  ZT_HIP(hipMemcpyAsync(ust.data(), d_ust, chain.size() * 4, hipMemcpyDeviceToHost, s));
-  std::vector<int32_t> st(segs.size());
-  ZT_HIP(hipMemcpyAsync(st.data(), d_st, segs.size() * 4, hipMemcpyDeviceToHost, s));
+  ZT_HIP(hipMemcpyAsync(h_ust, d_ust, chain.size() * 4, hipMemcpyDeviceToHost, s));
+  ZT_HIP(hipMemcpyAsync(h_st, d_st, segs.size() * 4, hipMemcpyDeviceToHost, s));
   ZT_HIP(hipStreamSynchronize(s));
   ZT_TRY(timing_collect(c, &c->times.inflate_ms, &c->times.inflate_launches, 2));
   ZT_TRY(timing_collect(c, &c->times.inflate_tok_ms, &c->times.inflate_toks, 3));
-  for (size_t i = 0; i < ust.size(); ++i)
-    if (ust[i] != ZT_OK) FALLBACK("unit %zu of %zu (chain): status %d\n", i, ust.size(), ust[i]);
-  for (size_t i = 0; i < st.size(); ++i)
-    if (st[i] != ZT_OK) FALLBACK("segment %zu of %zu: status %d\n", i, st.size(), st[i]);
+  for (size_t i = 0; i < chain.size(); ++i)
+    if (h_ust[i] != ZT_OK) FALLBACK("unit %zu of %zu (chain): status %d\n", i, chain.size(), h_ust[i]);
+  for (size_t i = 0; i < segs.size(); ++i)
+    if (h_st[i] != ZT_OK) FALLBACK("segment %zu of %zu: status %d\n", i, segs.size(), h_st[i]);
   return ZT_OK;
 }
 

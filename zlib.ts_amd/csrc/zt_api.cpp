@@ -105,20 +105,20 @@ int scratch(DeviceCtx *c, int slot, size_t bytes, void **ptr) {
   return ZT_OK;
 }
 
-int pinned(DeviceCtx *c, size_t bytes, void **ptr) {
+int pinned(DeviceCtx *c, size_t bytes, void **ptr, int slot) {
   if (bytes == 0) bytes = 16;
-  if (c->pinned_size < bytes) {
-    if (c->h_pinned) {
+  if (c->pinned_size[slot] < bytes) {
+    if (c->h_pinned[slot]) {
       ZT_HIP(hipDeviceSynchronize());
-      ZT_HIP(hipHostFree(c->h_pinned));
-      c->h_pinned = nullptr;
-      c->pinned_size = 0;
+      ZT_HIP(hipHostFree(c->h_pinned[slot]));
+      c->h_pinned[slot] = nullptr;
+      c->pinned_size[slot] = 0;
     }
     size_t sz = bytes + bytes / 4;
-    ZT_HIP(hipHostMalloc(&c->h_pinned, sz, hipHostMallocDefault));
-    c->pinned_size = sz;
+    ZT_HIP(hipHostMalloc(&c->h_pinned[slot], sz, hipHostMallocDefault));
+    c->pinned_size[slot] = sz;
   }
-  *ptr = c->h_pinned;
+  *ptr = c->h_pinned[slot];
   return ZT_OK;
 }
 

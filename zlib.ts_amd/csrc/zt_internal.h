@@ -44,12 +44,12 @@ struct DeviceCtx {
   // second stream: checksums run beside the deflate pipeline in the containers
   hipStream_t aux = nullptr;
   hipEvent_t aux_ev = nullptr;
-  void *h_pinned = nullptr;
+  void *h_pinned[2] = {};  // pinned host staging: 0 batch data, 1 inflate metadata
   // zt_timing_enable: HIP-event kernel timing
   bool timing = false;
   hipEvent_t ev[8] = {};  // [2k, 2k+1]: interval k (0 match, 1 deflate pipeline, 2 inflate)
   zt_kernel_times times = {};
-  size_t pinned_size = 0;
+  size_t pinned_size[2] = {};
 };
 
 // Records the begin / end event of interval k (0 or 1) when timing is on.
@@ -62,8 +62,8 @@ int timing_collect(DeviceCtx *c, double *acc_ms, uint64_t *count, int k = 0);
 int get_ctx(DeviceCtx **out);
 // Grow-only device scratch slot `slot` to at least `bytes`.
 int scratch(DeviceCtx *c, int slot, size_t bytes, void **ptr);
-// Grow-only pinned host staging buffer (one per context) of at least `bytes`.
-int pinned(DeviceCtx *c, size_t bytes, void **ptr);
+// Grow-only pinned host staging buffer `slot` (0 or 1) of at least `bytes`.
+int pinned(DeviceCtx *c, size_t bytes, void **ptr, int slot = 0);
 // fn(0 .. count-1) over a few host threads when total_bytes is large.
 void parallel_copy(size_t count, const std::function<void(size_t)> &fn, size_t total_bytes);
 
