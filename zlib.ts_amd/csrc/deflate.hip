@@ -76,6 +76,7 @@ struct DeflateParams {
   uint32_t blocks_per_wg;
   uint32_t nblocks;
   uint32_t restart;     // blocks per independent segment (multiple of blocks_per_wg)
+  uint32_t hist_max;    // history bytes a super-chunk loads (multiple of DF_SUB, <= DF_HIST)
   int final_;
   int max_chain;
   int nice_len;
@@ -472,7 +473,8 @@ __global__ __launch_bounds__(DF_THREADS) void match_kernel(DeflateParams P) {
   // the segment, so inflate can decode segments independently
   const bool restart = (b0 % P.restart) == 0 && (b0 > 0 || P.halo == 0);
   // history: whole sub-chunks, so that the searched range starts on a sub-chunk
-  const uint64_t hist = restart ? 0 : (s_lo < (uint64_t)DF_HIST ? (s_lo & ~uint64_t(DF_SUB - 1)) : DF_HIST);
+  const uint64_t hmax = P.hist_max;
+  const uint64_t hist = restart ? 0 : (s_lo < hmax ? (s_lo & ~uint64_t(DF_SUB - 1)) : hmax);
   const uint64_t h_lo = s_lo - hist;
   const uint8_t *g = P.base + h_lo;  // rel 0
   const uint32_t rs = (uint32_t)(s_lo - h_lo), re = (uint32_t)(s_hi - h_lo);
@@ -1881,6 +1883,10 @@ int deflate_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t halo, in
   P.blocks_per_wg = G.k;
   P.nblocks = G.nblocks;
   P.restart = (restart_blocks() + G.k - 1) / G.k * G.k;
+  // tuning hook: ZT_DF_HIST = KiB of history per super-chunk (multiple of 4, <= 28)
+  static const int hist_env = getenv("ZT_DF_HIST") ? atoi(getenv("ZT_DF_HIST")) : 0;
+  P.hist_max = hist_env > 0 && hist_env * 1024 <= DF_HIST && hist_env % 4 == 0 ? (uint32_t)hist_env * 1024u
+                                                                                : (uint32_t)DF_HIST;
   P.final_ = final_;
   const DeflateLevel L = level_params(level);
   P.max_chain = L.max_chain;
