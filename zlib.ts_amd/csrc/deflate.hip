@@ -49,7 +49,10 @@ __device__ unsigned long long g_bk_time[8];  // debug: block_kernel phase cycles
 __device__ unsigned long long g_df_count[4];  // debug: pair steps (per wave), lane hops, extends
 #endif
 
-constexpr int DF_BLOCK = 32768;
+#ifndef ZT_DF_BLOCK
+#define ZT_DF_BLOCK 32768
+#endif
+constexpr int DF_BLOCK = ZT_DF_BLOCK;
 constexpr int DF_SUB = 4096;
 constexpr int DF_RING = 32768;  // power of two: ring index = rel & (DF_RING - 1)
 constexpr int DF_SLOT = DF_BLOCK + DF_BLOCK / 8 + 1024;  // per-block slot: fits a forced fixed-code block
@@ -63,7 +66,7 @@ constexpr int DF_HIST = DF_RING - DF_SUB;     // 28672
 constexpr int DF_MAXDIST = DF_HIST - 64;      // 28608
 constexpr int ENC_THREADS = 256;
 // Independent segments of 1 MiB: restart points for segment-parallel inflate
-constexpr uint32_t kRestartBlocks = 32;
+constexpr uint32_t kRestartBlocks = (1u << 20) / DF_BLOCK;  // 1 MiB
 // empty head entry: p - kNoHead exceeds DF_MAXDIST for every rel position p
 constexpr uint32_t kNoHead = 0x80000000u;
 
@@ -1015,7 +1018,7 @@ __device__ uint32_t parse_block(S *s, ParseStage *st, const DeflateParams &P, ui
 // all lanes on the same row at the same step, so reads of one length l hit
 // distinct banks): differences over <= 258 positions stay below 2^15.
 typedef unsigned int op_u32x4 __attribute__((ext_vector_type(4)));
-constexpr int OP_SEG = 512;
+constexpr int OP_SEG = DF_BLOCK / 64;  // one segment per lane
 constexpr int OP_OV = 128;
 // C ring rows: C[i + l] for l <= OP_RING.  A longer match reads C[i + OP_RING]
 // instead of C[i + L] (an estimate of its continuation: the parse stays
@@ -1412,7 +1415,7 @@ __global__ __launch_bounds__(64) void block_kernel(DeflateParams P) {
   fix += 3;
   // stored: the block's bytes + 5 header bytes; Huffman forms add the
   // 3-bit marker header, padding and the 4 sync bytes
-  const uint64_t stored_bits = 8ull * (blen + 10);  // + its sync point
+  const uint64_t stored_bits = 8ull * (blen + 5 * ((blen + 65534) / 65535) + 5);  // + its sync point
   const uint64_t dyn_bits = ((dyn + 3 + 7) & ~7ull) + 32;
   const uint64_t fix_bits = ((fix + 3 + 7) & ~7ull) + 32;
   BK_T(4);
@@ -1601,21 +1604,27 @@ __global__ __launch_bounds__(ENC_THREADS) void encode_kernel(DeflateParams P) {
     const uint8_t *raw = P.base + P.halo + (uint64_t)blk * DF_BLOCK;
     // followed, like every block, by an empty stored block (the sync point
     // inflate splits on), which carries BFINAL on the stream's last block
+    // (pieces of at most 65535 bytes: a stored block's LEN is 16 bits)
+    const uint32_t nparts = blen ? (blen + 65534) / 65535 : 1;
+    if (t < nparts) {
+      const uint32_t plen = blen - t * 65535 < 65535 ? blen - t * 65535 : 65535;
+      uint8_t *h = slot_bytes + (size_t)t * (65535 + 5);
+      h[0] = 0;
+      h[1] = plen & 0xFF;
+      h[2] = plen >> 8;
+      h[3] = (~plen) & 0xFF;
+      h[4] = ((~plen) >> 8) & 0xFF;
+    }
     if (t == 0) {
-      slot_bytes[0] = 0;
-      slot_bytes[1] = blen & 0xFF;
-      slot_bytes[2] = blen >> 8;
-      slot_bytes[3] = (~blen) & 0xFF;
-      slot_bytes[4] = ((~blen) >> 8) & 0xFF;
-      uint8_t *e = slot_bytes + 5 + blen;
+      uint8_t *e = slot_bytes + 5 * nparts + blen;
       e[0] = last ? 1 : 0;
       e[1] = 0;
       e[2] = 0;
       e[3] = 0xFF;
       e[4] = 0xFF;
-      P.slot_len[blk] = blen + 10;
+      P.slot_len[blk] = blen + 5 * nparts + 5;
     }
-    for (uint32_t i = t; i < blen; i += ENC_THREADS) slot_bytes[5 + i] = raw[i];
+    for (uint32_t i = t; i < blen; i += ENC_THREADS) slot_bytes[5 * (i / 65535 + 1) + i] = raw[i];
     return;
   }
   for (uint32_t i = t; i < 288; i += ENC_THREADS) s->lit_code[i] = plan->lit_code[i];
@@ -1825,7 +1834,7 @@ static size_t deflate_geometry(const DeviceCtx *c, size_t n, DeflateGeom *g) {
   uint32_t kk = (g->nblocks + 2 * c->num_cu - 1) / (2 * c->num_cu);
   // tuning hook: ZT_DF_SUPER caps the blocks per workgroup (power of two <= 32)
   static const int cap_env = getenv("ZT_DF_SUPER") ? atoi(getenv("ZT_DF_SUPER")) : 0;
-  const uint32_t cap = cap_env > 0 && cap_env <= 32 ? (uint32_t)cap_env : 4u;
+  const uint32_t cap = cap_env > 0 && cap_env <= 32 ? (uint32_t)cap_env : (uint32_t)((128u << 10) / DF_BLOCK);
   uint32_t k2 = 1;
   while (k2 < kk && k2 < cap) k2 <<= 1;
   g->k = k2;
@@ -1842,12 +1851,12 @@ static size_t deflate_geometry(const DeviceCtx *c, size_t n, DeflateGeom *g) {
 // up to a multiple of the blocks per workgroup)
 static uint32_t restart_blocks() {
   static const int e = getenv("ZT_DF_RESTART") ? atoi(getenv("ZT_DF_RESTART")) : 0;
-  return e >= 8 ? (uint32_t)e : kRestartBlocks;
+  return e >= 4 ? (uint32_t)e : kRestartBlocks;
 }
 
 size_t deflate_bound_bytes(size_t n) {
   size_t nb = (n + DF_BLOCK - 1) / DF_BLOCK;
-  return n + nb * 16 + (nb / 8 + 1) * kRestartMarkerLen + 64;
+  return n + nb * 16 + (nb / 4 + 1) * kRestartMarkerLen + 64;
 }
 
 int deflate_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t halo, int final_, int ctype, int level,

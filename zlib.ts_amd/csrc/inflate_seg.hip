@@ -46,7 +46,10 @@ bool inf_debug() {
     if (inf_debug()) fprintf(stderr, "[zt inflate] " __VA_ARGS__); \
     return 1;                                           \
   } while (0)
-constexpr uint32_t kUnitTokCap = 32768 + 64;  // a 32 KiB block has <= 32768 tokens
+#ifndef ZT_DF_BLOCK
+#define ZT_DF_BLOCK 32768
+#endif
+constexpr uint32_t kUnitTokCap = ZT_DF_BLOCK + 64;  // this engine's units are one block: <= 1 token per byte
 
 // sync point = byte after an aligned 00 00 FF FF; list entry = pos << 1 | restart
 // One 16-byte aligned chunk per lane, loaded as one 16-byte word; the 8 bytes
