@@ -760,8 +760,17 @@ __global__ __launch_bounds__(64) void expand_kernel(ResolveParams P) {
 
 typedef unsigned int u32x4r __attribute__((ext_vector_type(4)));
 
-constexpr uint32_t CP_DESC_RING = 2048;  // descriptors staged in LDS (16 chunks of 128)
-constexpr uint32_t CP_AHEAD = 12;
+#ifndef ZT_CP_RING
+#define ZT_CP_RING 2048
+#endif
+#ifndef ZT_CP_AHEAD
+#define ZT_CP_AHEAD 12
+#endif
+constexpr uint32_t CP_DESC_RING = ZT_CP_RING;  // descriptors staged in LDS (chunks of 128)
+constexpr uint32_t CP_AHEAD = ZT_CP_AHEAD;      // chunks in flight ahead of the step
+static_assert((CP_AHEAD + 2) * 128 <= CP_DESC_RING && CP_AHEAD < 64, "descriptor ring");
+// s_waitcnt vmcnt(v) with lgkmcnt / expcnt left alone (vmcnt bits 3:0 and 15:14)
+constexpr int cp_vmcnt(uint32_t v) { return (int)(0x0F70u | (v & 15u) | ((v >> 4) << 14)); }
 
 struct CopyShared {
   uint8_t ring[RING];                        // 32 KiB history, also the output staging
@@ -810,7 +819,7 @@ __global__ __launch_bounds__(64) void copy_kernel(ResolveParams P) {
       ++issued;
     }
     if (issued - need >= CP_AHEAD)
-      __builtin_amdgcn_s_waitcnt(0x0F70 | CP_AHEAD);
+      __builtin_amdgcn_s_waitcnt(cp_vmcnt(CP_AHEAD));
     else
       __builtin_amdgcn_s_waitcnt(0x0F70);
     // lane j: bytes op + 4 j .. op + 4 j + 3 (bytes past n are never flushed)
