@@ -789,11 +789,13 @@ __device__ __forceinline__ void cp_flush(const CopyShared *sh, uint8_t *out, uin
 }
 
 // one descriptor -> byte, or -1 for "the byte op + off of this step"
+// (branch-free: the ring is read for every descriptor, the literal selected
+// after -- per-byte branches cost more issue slots than the extra LDS read)
 __device__ __forceinline__ uint32_t cp_byte(const CopyShared *sh, uint64_t op, uint32_t d, int32_t &off) {
-  off = -1;
-  if (!(d & 0x8000u)) return sh->ring[(op - d - 1) & RING_MASK];
-  if (d & 0x100u) off = (int32_t)(d & 0xFF);
-  return d & 0xFF;
+  const uint32_t rv = sh->ring[((uint32_t)op - d - 1) & RING_MASK];
+  const bool lit = (d & 0x8000u) != 0;
+  off = (lit && (d & 0x100u)) ? (int32_t)(d & 0xFF) : -1;
+  return lit ? (d & 0xFF) : rv;
 }
 
 __global__ __launch_bounds__(64) void copy_kernel(ResolveParams P) {
