@@ -825,7 +825,7 @@ __global__ __launch_bounds__(64) void copy_kernel(ResolveParams P) {
     else
       __builtin_amdgcn_s_waitcnt(0x0F70);
     // lane j: bytes op + 4 j .. op + 4 j + 3 (bytes past n are never flushed)
-    const uint64_t x = op + 4 * (uint64_t)lane;
+    const uint32_t x = (uint32_t)op + 4 * (uint32_t)lane;  // ring / descriptor index (masked)
     const uint64_t dd = *reinterpret_cast<const uint64_t *>(&sh.desc[x & (CP_DESC_RING - 1)]);
     int32_t o0, o1, o2, o3;
     const uint32_t b0 = cp_byte(&sh, op, (uint32_t)dd & 0xFFFF, o0);
