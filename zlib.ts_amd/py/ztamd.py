@@ -191,9 +191,10 @@ def inflate_raw(data, index=0, ref_strict=False, buffer_type=1, buffer_size=0x80
 def inflate_raw_batch(streams, ref_strict=False):
     """Returns a list of (status, output bytes, end ip)."""
     k = len(streams)
-    bufs = [_cbuf(s) for s in streams]
-    ptrs = (ctypes.c_void_p * k)(*[ctypes.addressof(b) for b, _ in bufs])
-    lens = (ctypes.c_size_t * k)(*[n for _, n in bufs])
+    # the bytes objects' own buffers are passed (no copy); `bs` keeps them alive
+    bs = [bytes(x) for x in streams]
+    ptrs = (ctypes.c_void_p * k)(*[ctypes.cast(ctypes.c_char_p(x), ctypes.c_void_p).value for x in bs])
+    lens = (ctypes.c_size_t * k)(*[len(x) for x in bs])
     outs = (ctypes.POINTER(ctypes.c_uint8) * k)()
     olens = (ctypes.c_size_t * k)()
     ips = (ctypes.c_size_t * k)()
