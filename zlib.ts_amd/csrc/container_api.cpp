@@ -43,6 +43,7 @@ int deflate_with_checksums(const uint8_t *in, size_t n, const zt_deflate_opts *o
                            uint32_t *adler) {
   DeviceCtx *c;
   ZT_TRY(get_ctx(&c));
+  std::lock_guard<std::recursive_mutex> ctx_lock(c->mu);
   int ct, lv;
   ZT_TRY(resolve_deflate(opts, &ct, &lv));
   const size_t ob = (ct == 0 ? n + 5 * ((n + 65534) / 65535) + 16 : deflate_bound_bytes(n) + (ct == 1 ? n / 8 + 64 : 0));

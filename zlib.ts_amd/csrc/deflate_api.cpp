@@ -57,6 +57,7 @@ int zt_deflate_plan_create(size_t max_n, const zt_deflate_opts *opts, zt_deflate
   if (!plan) return set_error(ZT_E_ARG, "null plan");
   DeviceCtx *c;
   ZT_TRY(get_ctx(&c));
+  std::lock_guard<std::recursive_mutex> ctx_lock(c->mu);
   int ct, lv;
   ZT_TRY(resolve(opts, &ct, &lv));
   zt_deflate_plan *p = new zt_deflate_plan();
@@ -86,6 +87,7 @@ int zt_deflate_dev(zt_deflate_plan *plan, const void *d_in, size_t n, size_t hal
   if (n > plan->max_n) return set_error(ZT_E_ARG, "input larger than the plan");
   DeviceCtx *c;
   ZT_TRY(get_ctx(&c));
+  std::lock_guard<std::recursive_mutex> ctx_lock(c->mu);
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   if (halo > 32768) halo = 32768;
   return deflate_dev_run(c, (const uint8_t *)d_in, n, halo, final_, plan->ctype, plan->level, (uint8_t *)d_out,
@@ -97,6 +99,7 @@ int zt_deflate_raw(const uint8_t *in, size_t n, const zt_deflate_opts *opts, uin
   if (n && !in) return set_error(ZT_E_ARG, "null input");
   DeviceCtx *c;
   ZT_TRY(get_ctx(&c));
+  std::lock_guard<std::recursive_mutex> ctx_lock(c->mu);
   int ct, lv;
   ZT_TRY(resolve(opts, &ct, &lv));
   const size_t ob = out_bound(ct, n);
@@ -132,6 +135,7 @@ int zt_inflate_plan_create(size_t max_in, size_t max_out, zt_inflate_plan **plan
   if (!plan) return set_error(ZT_E_ARG, "null plan");
   DeviceCtx *c;
   ZT_TRY(get_ctx(&c));
+  std::lock_guard<std::recursive_mutex> ctx_lock(c->mu);
   zt_inflate_plan *p = new zt_inflate_plan();
   p->device = c->device;
   p->max_in = max_in;
@@ -156,6 +160,7 @@ int zt_inflate_dev(zt_inflate_plan *plan, const void *d_in, size_t n, void *d_ou
   if (!plan || !out_len) return set_error(ZT_E_ARG, "null argument");
   DeviceCtx *c;
   ZT_TRY(get_ctx(&c));
+  std::lock_guard<std::recursive_mutex> ctx_lock(c->mu);
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   uint8_t *o = (uint8_t *)d_out;
   size_t ol = 0, eip = 0;

@@ -175,6 +175,7 @@ static int inflate_host_batch(const uint8_t *const *in, const size_t *n, const s
                               int *status) {
   DeviceCtx *c;
   ZT_TRY(get_ctx(&c));
+  std::lock_guard<std::recursive_mutex> ctx_lock(c->mu);
   const int strict = opts ? opts->ref_strict : 0;
   std::vector<size_t> in_off(count), cap(count);
   size_t in_total = 0;
@@ -291,6 +292,7 @@ int zt_inflate_raw(const uint8_t *in, size_t n, size_t index, const zt_inflate_o
     // large stream: segment-parallel decode when it carries restart points
     DeviceCtx *c;
     ZT_TRY(get_ctx(&c));
+    std::lock_guard<std::recursive_mutex> ctx_lock(c->mu);
     void *d_in;
     ZT_TRY(scratch(c, 0, n, &d_in));
     ZT_HIP(hipMemcpyAsync(d_in, in, n, hipMemcpyHostToDevice, c->stream));

@@ -92,6 +92,7 @@ extern "C" int zt_synth_dev(int kind, uint32_t seed, void *d_out, size_t n, void
   if (reinterpret_cast<uintptr_t>(d_out) & 3) return set_error(ZT_E_ARG, "output must be 4-byte aligned");
   DeviceCtx *c;
   ZT_TRY(get_ctx(&c));
+  std::lock_guard<std::recursive_mutex> ctx_lock(c->mu);
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   const uint64_t pieces = (n + kPieceBytes - 1) / kPieceBytes;
   synth_kernel<<<(unsigned)((pieces + 63) / 64), 64, 0, s>>>(kind, seed, static_cast<uint8_t *>(d_out), n);

@@ -168,6 +168,7 @@ int zt_dev_checksums(const void *d_in, size_t n, uint32_t crc_in, uint32_t adler
                      uint32_t *adler_out, void *stream) {
   DeviceCtx *c;
   ZT_TRY(get_ctx(&c));
+  std::lock_guard<std::recursive_mutex> ctx_lock(c->mu);
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   if (n == 0) {
     if (crc_out) *crc_out = crc_in;
@@ -190,6 +191,7 @@ static int checksums_host(const uint8_t *data, size_t len, uint32_t crc_in, uint
                           uint32_t *adler_out) {
   DeviceCtx *c;
   ZT_TRY(get_ctx(&c));
+  std::lock_guard<std::recursive_mutex> ctx_lock(c->mu);
   if (len == 0) {  // the reference returns its inputs untouched (no % 65521)
     if (crc_out) *crc_out = crc_in;
     if (adler_out) *adler_out = adler_in;
@@ -220,6 +222,7 @@ int zt_checksums(const uint8_t *data, size_t len, uint32_t crc_in, uint32_t adle
 int zt_timing_enable(int on) {
   DeviceCtx *c;
   ZT_TRY(get_ctx(&c));
+  std::lock_guard<std::recursive_mutex> ctx_lock(c->mu);
   c->timing = on != 0;
   c->times = zt_kernel_times{};
   return ZT_OK;
@@ -229,6 +232,7 @@ int zt_timing_read(zt_kernel_times *out) {
   if (!out) return set_error(ZT_E_ARG, "null output");
   DeviceCtx *c;
   ZT_TRY(get_ctx(&c));
+  std::lock_guard<std::recursive_mutex> ctx_lock(c->mu);
   *out = c->times;
   return ZT_OK;
 }

@@ -1,6 +1,7 @@
 // zt_internal.h -- shared host/device helpers for libzt (not installed).
 #pragma once
 #include <functional>
+#include <mutex>
 #include <hip/hip_runtime.h>
 
 #include <cstddef>
@@ -31,6 +32,9 @@ int hip_fail(hipError_t e, const char *what);
 // One default stream per device plus grow-only scratch buffers, so the
 // host-pointer entry points do not hipMalloc on every call.
 struct DeviceCtx {
+  // host entry points hold it for their whole call: scratch, pinned staging
+  // and the streams are shared by every thread that uses this device
+  std::recursive_mutex mu;
   int device = -1;
   hipStream_t stream = nullptr;
   int num_cu = 0;
