@@ -1,6 +1,7 @@
 #!/bin/bash
 # Build libzt.so with extra compile flags into build/var_NAME/ (tuning experiments;
 # load it with ZT_LIB=...).   usage: tools/build_variant.sh NAME FLAGS...
+# build/var_* is listed in .gpurunignore: drop that line while sweeping variants on the GPU.
 set -e
 NAME=$1; shift
 cd "$(dirname "$0")/../zlib.ts_amd"
