@@ -32,6 +32,8 @@ struct HuffTab {
   uint32_t count[16];
   uint32_t offs[16];
   uint32_t running[16];
+  uint64_t lim[16];   // (first + count) << (32 - l): left-justified end of the length-l codes
+  int32_t base[16];   // offs - first: sorted[] index of a code of length l is base + code
   int maxlen;
   int status;
 };
@@ -80,6 +82,10 @@ __device__ __forceinline__ int build_table(const uint8_t *lens, int n, HuffTab *
     }
     t->first[0] = 0;
     t->offs[0] = 0;
+    for (int l = 1; l < 16; ++l) {
+      t->lim[l] = (uint64_t)(t->first[l] + t->count[l]) << (32 - l);
+      t->base[l] = (int32_t)t->offs[l] - (int32_t)t->first[l];
+    }
     t->maxlen = maxlen;
     t->status = st;
   }

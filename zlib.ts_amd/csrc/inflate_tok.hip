@@ -208,18 +208,17 @@ struct LaneBits {
 };
 
 // code longer than PRI bits, per lane
+// (canonical limits: the length is one more than the number of lengths
+// whose left-justified code range ends at or below the peek; all limits are
+// read at once instead of a length-by-length search)
 __device__ __forceinline__ int long_code_lane(const HuffTab *t, uint32_t v, uint32_t &len) {
-  const uint32_t r = __brev(v);
-  const int ml = t->maxlen;
-  for (int l = PRI + 1; l <= ml; ++l) {
-    const uint32_t c = r >> (32 - l);
-    const uint32_t k = c - t->first[l];
-    if (k < t->count[l]) {
-      len = (uint32_t)l;
-      return (int)t->sorted[t->offs[l] + k];
-    }
-  }
-  return -1;
+  const uint64_t r = __brev(v);
+  uint32_t l = PRI + 1;
+#pragma unroll
+  for (int k = PRI + 1; k < 16; ++k) l += r >= t->lim[k] ? 1u : 0u;
+  if (l > (uint32_t)t->maxlen) return -1;
+  len = l;
+  return (int)t->sorted[t->base[l] + (int32_t)((uint32_t)r >> (32 - l))];
 }
 
 // one token at the lane's position: 0 ok (tok, nbytes), 1 end of block, -1 invalid
