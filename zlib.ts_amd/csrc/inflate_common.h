@@ -306,20 +306,16 @@ __device__ __forceinline__ int decode_sym(Reader &rd, const HuffTab *t, int &cle
     len = (int)(e & 15);
     sym = (int)((e >> 8) & 511);
   } else {
-    uint32_t r = __brev(v);
-    len = 0;
-    sym = -1;
-    const int ml = (int)uni((uint32_t)t->maxlen);
-    for (int l = PRI + 1; l <= ml; ++l) {
-      uint32_t c = r >> (32 - l);
-      uint32_t k = c - uni(t->first[l]);
-      if (k < uni(t->count[l])) {
-        len = l;
-        sym = (int)uni(t->sorted[uni(t->offs[l]) + k]);
-        break;
-      }
-    }
-    if (sym < 0) return ZT_E_INVALID_SYMBOL;  // bits match no code of an incomplete set
+    // canonical limits (see HuffTab::lim): the length is one more than the
+    // number of lengths whose code range ends at or below the peek
+    const uint64_t r = __brev(v);
+    uint32_t l = PRI + 1;
+#pragma unroll
+    for (int k = PRI + 1; k < 16; ++k) l += r >= t->lim[k] ? 1u : 0u;
+    l = uni(l);
+    if (l > (uint32_t)uni((uint32_t)t->maxlen)) return ZT_E_INVALID_SYMBOL;  // bits match no code of an incomplete set
+    len = (int)l;
+    sym = (int)uni(t->sorted[t->base[l] + (int32_t)((uint32_t)r >> (32 - l))]);
   }
   clen = len;
   if (rd.past_end((uint32_t)len)) return ZT_E_INVALID_CODE_LENGTH;
