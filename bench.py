@@ -10,36 +10,136 @@ The corpus is SURVEY.md 8(d)'s mixed generator set (wordsalad, xorshift32,
 structured int32 deltas, cycling per 4 MiB window), generated on the device.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--size BYTES] [--level L]
+                  [--mode weak|c3]
 
-For N > 1 the driver launches one process per GPU (torch.distributed.run);
-every rank round-trips its own 1 GiB buffer (weak scaling, no collective on
-the data path); the timed region is bracketed by barrier + synchronize and
-the maximum over ranks is reported.  value = total bytes round-tripped by all
-ranks / max elapsed.
+Processes: one per GPU.  Under torch.distributed.run (WORLD_SIZE set) every
+process is one rank.  `--gpus N` without a launcher makes this process a
+plain launcher: it starts N rank processes of itself (subprocess, before any
+GPU call here) with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, and exits
+with their worst status.  Rank r uses device r % device_count (so N ranks can
+be rehearsed on a one-GPU box).  Ranks meet over gloo (host TCP): the data
+path has no collective at all; gloo carries the barriers
+around the timed region, the max-over-ranks of the elapsed time, and the
+sums for the ratio.
+
+Modes:
+  weak  (default) every rank round-trips its own `--size` buffer (1 GiB):
+        value = total bytes of all ranks / max elapsed, "scaling": "weak".
+  c3    config C3: ONE `--size` buffer (default 8 GiB) split by
+        zt_shard.shard_range into segment-aligned shards, one per rank, each
+        generated in place (zt_synth_dev_at), deflated with final only on the
+        last rank; the shards' streams concatenate into one valid stream.  A
+        step is the deflate of the whole buffer; value = buffer bytes / max
+        elapsed, "scaling": "strong".  Each rank checks its shard by inflating
+        its stream (closed by an empty final block when not last) on device.
 
 Extra fields: `roofline` for the dominant kernel (deflate's match_kernel,
 the LZ77 match finder; algorithmic bytes = N input bytes per launch, SURVEY.md
-8(d), timed with HIP events on its launch stream), `cpu_baseline` (the oracle -- the
-C restatement of the reference's RawDeflate + RawInflate -- on a bounded
-sample, rank 0, N = 1 only), and the per-generator compression ratio of this
-build against the reference on that sample.
+8(d), timed with HIP events on its launch stream), `cpu_baseline` (the oracle
+-- the C restatement of the reference's RawDeflate + RawInflate -- on a
+bounded sample, rank 0, N = 1 only), the per-generator compression ratio of
+this build against the reference on that sample, and `api` -- the same round
+trip through the host-buffer entry points (zt_deflate_raw / zt_inflate_raw),
+PCIe transfers included (rank 0, N = 1, weak mode only).
 """
 import argparse
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "zlib.ts_amd", "py"))
 
-import torch  # noqa: E402
-
-from zt_shard import max_over_ranks  # noqa: E402
-
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 WINDOW = 4 << 20
 KINDS = ["wordsalad", "xorshift32", "structured"]  # mixed corpus order per 4 MiB window
+METRIC = "GiB/s RawDeflate L6 + RawInflate on 1 GiB buffer; ratio vs ref"
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--size", type=int, default=None, help="bytes (default 1 GiB; 8 GiB in c3 mode)")
+    ap.add_argument("--level", type=int, default=6)
+    ap.add_argument("--mode", choices=["weak", "c3"], default="weak")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-api", action="store_true", help="skip the host-buffer (PCIe-inclusive) round trip")
+    a = ap.parse_args(argv)
+    if a.size is None:
+        a.size = (8 << 30) if a.mode == "c3" else (1 << 30)
+    return a
+
+
+# ---------------------------------------------------------------- launcher
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch(nproc):
+    """Start `nproc` rank processes of this script and wait for them.  Runs
+    before anything in this process touches the GPU."""
+    port = str(_free_port())
+    procs = []
+    for r in range(nproc):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nproc), LOCAL_WORLD_SIZE=str(nproc),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    for p in procs:
+        rc = max(rc, p.wait())
+    return rc
+
+
+# ---------------------------------------------------------------- helpers
+def source_digest():
+    """sha256 of the libzt sources (zlib.ts_amd/csrc, include/zt.h): ties a
+    PMC traffic measurement to the kernels it was taken on."""
+    h = hashlib.sha256()
+    d = os.path.join(HERE, "zlib.ts_amd", "csrc")
+    for f in sorted(os.listdir(d)) + ["../../include/zt.h"]:
+        with open(os.path.join(d, f), "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    return h.hexdigest()
+
+
+def pmc_traffic(kernel, n):
+    """HBM bytes per launch of `kernel` from profiles/pmc_traffic.json
+    (tools/pmc_traffic.py over rocprofv3 FETCH_SIZE / WRITE_SIZE passes of
+    this workload), or None when the file was measured on other kernel
+    sources or another size: a stale measurement is never reported."""
+    path = os.path.join(HERE, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        k = d["kernels"][kernel]
+    except (OSError, KeyError, ValueError):
+        return None
+    if n != 1 << 30 or d.get("source_sha256") != source_digest():
+        return None
+    return int(k["traffic_bytes"])
+
+
+def host_info():
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return os.cpu_count(), model
 
 
 def cpu_baseline(d_in, level, zt):
@@ -63,6 +163,7 @@ def cpu_baseline(d_in, level, zt):
         nbytes += len(chunk)
         ours = zt.deflate_raw(chunk, level=level)
         ratios[kind] = round(len(ours) / len(ref), 4)
+    nproc, model = host_info()
     return {
         "value": round(nbytes / t_total / 2**30, 5),
         "unit": "GiB/s",
@@ -70,73 +171,122 @@ def cpu_baseline(d_in, level, zt):
         "kind": "port",
         "sample": "RawDeflate (reference defaults) + RawInflate of the first 3 x 4 MiB windows of the corpus "
                   "(wordsalad, xorshift32, structured), oracle/liboracle.so, single thread",
+        "host_nproc": nproc,
+        "host_cpu_model": model,
     }, ratios
 
 
-def pmc_traffic(kernel, n):
-    """HBM bytes per launch of `kernel` measured by rocprofv3 PMC passes
-    (FETCH_SIZE x2 + WRITE_SIZE, tools/pmc_traffic.py) on this workload, or
-    None when no measurement for this size is committed."""
-    path = os.path.join(HERE, "profiles", "pmc_traffic.json")
-    try:
-        with open(path) as f:
-            k = json.load(f)["kernels"][kernel]
-    except (OSError, KeyError, ValueError):
-        return None
-    if n != 1 << 30:
-        return None
-    return int(k["traffic_bytes"])
+def api_roundtrip(d_in, n, level, zt):
+    """The round trip through the host-buffer entry points (what a Node
+    caller of RawDeflate / RawInflate runs): zt_deflate_raw of a host copy of
+    the corpus, then zt_inflate_raw of the host stream, each C call timed
+    (PCIe transfers, pinning and host output allocation included)."""
+    import ctypes
+
+    import numpy as np
+
+    host = d_in.cpu().numpy()
+    src = host.ctypes.data_as(ctypes.c_void_p)
+    opts = zt.DeflateOpts(2, 0, level)
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    olen = ctypes.c_size_t()
+    zt._check(zt.lib.zt_deflate_raw(src, n, ctypes.byref(opts), ctypes.byref(out), ctypes.byref(olen)))  # warm
+    zt.lib.zt_free(out)
+    t0 = time.perf_counter()
+    zt._check(zt.lib.zt_deflate_raw(src, n, ctypes.byref(opts), ctypes.byref(out), ctypes.byref(olen)))
+    t_def = time.perf_counter() - t0
+    iopts = zt.InflateOpts(1, 0x8000, 0)
+    back = ctypes.POINTER(ctypes.c_uint8)()
+    blen, ip = ctypes.c_size_t(), ctypes.c_size_t()
+    t0 = time.perf_counter()
+    zt._check(zt.lib.zt_inflate_raw(out, olen.value, 0, ctypes.byref(iopts), ctypes.byref(back), ctypes.byref(blen),
+                                    ctypes.byref(ip)))
+    t_inf = time.perf_counter() - t0
+    ok = blen.value == n and np.array_equal(np.ctypeslib.as_array(back, shape=(n,)), host)
+    zt.lib.zt_free(back)
+    zt.lib.zt_free(out)
+    if not ok:
+        raise SystemExit("bench: host API round trip mismatch")
+    g = n / 2**30
+    return {"deflate_GiBps": round(g / t_def, 3), "inflate_GiBps": round(g / t_inf, 3),
+            "roundtrip_GiBps": round(g / (t_def + t_inf), 3),
+            "note": "zt_deflate_raw + zt_inflate_raw on pageable host buffers, PCIe and host allocation included"}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--size", type=int, default=1 << 30)
-    ap.add_argument("--level", type=int, default=6)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    args = ap.parse_args()
+# ---------------------------------------------------------------- ranks
+def run_rank(args):
+    import torch
+    import torch.distributed as dist
+
+    from zt_shard import max_over_ranks, shard_range, sum_over_ranks
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    ndev = torch.cuda.device_count()
+    if ndev == 0:
+        raise SystemExit("bench: no GPU visible")
+    dev = local % ndev
+    torch.cuda.set_device(dev)
     import ztamd as zt
 
-    zt.set_device(local)
-    dist = None
+    zt.set_device(dev)
+    pg = None
     if world > 1:
-        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        pg = dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-
-    n = args.size
-    d_in = torch.empty(n, dtype=torch.uint8, device="cuda")
-    zt.synth_dev("mixed", 11 + 7919 * rank, d_in.data_ptr(), n)
-    bound = zt.deflate_bound(n)
-    d_c = torch.empty(bound, dtype=torch.uint8, device="cuda")
-    d_out = torch.empty(n + 4096, dtype=torch.uint8, device="cuda")
-    dplan = zt.DeflatePlan(n, level=args.level)
-    iplan = zt.InflatePlan(bound, n)
+    if args.mode == "c3":
+        total = args.size
+        lo, hi = shard_range(total, world, rank)
+        n = hi - lo
+        last = rank == world - 1
+    else:
+        total = args.size * world
+        lo, n, last = 0, args.size, True
+    nalloc = max(1, n)
+    d_in = torch.empty(nalloc + 64, dtype=torch.uint8, device="cuda")
+    if args.mode == "c3":
+        zt.synth_dev_at("mixed", 11, lo, d_in.data_ptr(), n)
+    else:
+        zt.synth_dev("mixed", 11 + 7919 * rank, d_in.data_ptr(), n)
+    bound = zt.deflate_bound(nalloc)
+    d_c = torch.empty(bound + 64, dtype=torch.uint8, device="cuda")
+    d_out = torch.empty(nalloc + 4096, dtype=torch.uint8, device="cuda")
+    dplan = zt.DeflatePlan(nalloc, level=args.level)
+    iplan = zt.InflatePlan(bound + 64, nalloc)
     torch.cuda.synchronize()
+
+    def deflate():
+        return dplan.run(d_in.data_ptr(), n, d_c.data_ptr(), halo=0, final=1 if last else 0) if n else 0
+
+    def inflate(clen):
+        olen, _ = iplan.run(d_c.data_ptr(), clen, d_out.data_ptr(), d_out.numel())
+        return olen
 
     def step():
-        clen = dplan.run(d_in.data_ptr(), n, d_c.data_ptr())
-        olen, _ = iplan.run(d_c.data_ptr(), clen, d_out.data_ptr(), d_out.numel())
-        return clen, olen
+        clen = deflate()
+        if args.mode == "c3":
+            return clen, None
+        return clen, inflate(clen)
 
     # correctness of the measured path (untimed): the round trip is exact
-    clen, olen = step()
-    torch.cuda.synchronize()
-    if olen != n or not torch.equal(d_out[:n], d_in):
-        raise SystemExit("bench: round trip mismatch")
+    clen = deflate()
+    if n:
+        slen = clen
+        if not last:  # close this shard's stream with an empty final fixed block (03 00)
+            d_c[clen:clen + 2] = torch.tensor([3, 0], dtype=torch.uint8, device="cuda")
+            slen += 2
+        olen = inflate(slen)
+        torch.cuda.synchronize()
+        if olen != n or not torch.equal(d_out[:n], d_in[:n]):
+            raise SystemExit(f"bench: round trip mismatch on rank {rank}")
     for _ in range(args.warmup):
         step()
 
     def barrier():
-        if dist is not None:
-            dist.barrier()
+        if pg is not None:
+            pg.barrier()
 
     barrier()
     torch.cuda.synchronize()
@@ -149,17 +299,28 @@ def main():
     elapsed = time.perf_counter() - t0
     kt = zt.timing_read()
     zt.timing_enable(False)
-    elapsed = max_over_ranks(elapsed, dist, device="cuda")
+    elapsed = max_over_ranks(elapsed, pg)
+    total_c = sum_over_ranks(clen, pg)
 
-    value = world * n * args.steps / elapsed / 2**30
+    value = total * args.steps / elapsed / 2**30
     ms_step = elapsed / args.steps * 1e3
     def_ms = kt["deflate_ms"] / max(1, kt["deflate_launches"])  # match_kernel (dominant deflate kernel)
     pipe_ms = kt["deflate_pipeline_ms"] / max(1, kt["deflate_pipelines"])
     inf_ms = kt["inflate_ms"] / max(1, kt["inflate_launches"])
     tok_ms = kt["inflate_tok_ms"] / max(1, kt["inflate_toks"])
     achieved = n / (def_ms * 1e-3) / 1e9 if def_ms > 0 else 0.0
+    if args.mode == "c3":
+        workload = (f"config C3: RawDeflate level {args.level} of one {total / 2**30:g} GiB device-resident buffer "
+                    f"sharded over {world} GPU(s) (segment-aligned shards, streams concatenate)")
+        parallelism = f"shard x{world} (no collective)"
+        metric = "GiB/s RawDeflate L6 of one sharded buffer (config C3); ratio vs ref"
+    else:
+        workload = (f"RawDeflate level {args.level} + RawInflate round trip of a {n / 2**30:g} GiB "
+                    "device-resident buffer per GPU")
+        parallelism = f"batch split x{world} (no collective)"
+        metric = METRIC
     line = {
-        "metric": "GiB/s RawDeflate L6 + RawInflate on 1 GiB buffer; ratio vs ref",
+        "metric": metric,
         "value": round(value, 4),
         "unit": "GiB/s",
         "n_gpus": world,
@@ -167,34 +328,44 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_step, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.mode == "c3" else "weak",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (device-generated mixed corpus: wordsalad / xorshift32 / structured per 4 MiB window)",
-        "config": {"workload": f"RawDeflate level {args.level} + RawInflate round trip of a {n / 2**30:g} GiB "
-                               "device-resident buffer per GPU", "bytes_per_gpu": n, "level": args.level,
-                   "parallelism": f"batch split x{world} (no collective)"},
-        "ratio": round(clen / n, 5),
+        "config": {"workload": workload, "bytes_total": total, "level": args.level, "parallelism": parallelism},
+        "ratio": round(total_c / max(1, total), 5),
         "match_kernel_ms": round(def_ms, 3),
         "deflate_pipeline_ms": round(pipe_ms, 3),
-        "inflate_kernel_ms": round(inf_ms, 3),
-        "inflate_tokenize_ms": round(tok_ms, 3),
         "deflate_GiBps": round(n / (pipe_ms * 1e-3) / 2**30, 3) if pipe_ms else None,
-        "inflate_GiBps": round(n / (inf_ms * 1e-3) / 2**30, 3) if inf_ms else None,
         "roofline": {"bound": "hbm", "kernel": "match_kernel", "achieved": round(achieved, 3),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
                      "traffic": pmc_traffic("match_kernel", n)},
+        "devices_visible": ndev,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and n >= 3 * WINDOW:
-        cb, ratios = cpu_baseline(d_in, args.level, zt)
-        line["cpu_baseline"] = cb
-        line["ratio_vs_ref"] = ratios
+    if args.mode != "c3":
+        line["inflate_kernel_ms"] = round(inf_ms, 3)
+        line["inflate_tokenize_ms"] = round(tok_ms, 3)
+        line["inflate_GiBps"] = round(n / (inf_ms * 1e-3) / 2**30, 3) if inf_ms else None
+    if rank == 0 and world == 1 and args.mode == "weak":
+        if not args.no_cpu_baseline and n >= 3 * WINDOW:
+            cb, ratios = cpu_baseline(d_in, args.level, zt)
+            line["cpu_baseline"] = cb
+            line["ratio_vs_ref"] = ratios
+        if not args.no_api:
+            line["api"] = api_roundtrip(d_in[:n], n, args.level, zt)
     if rank == 0:
         print(json.dumps(line), flush=True)
     dplan.close()
     iplan.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    if pg is not None:
+        pg.destroy_process_group()
+
+
+def main():
+    args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch(args.gpus))
+    run_rank(args)
 
 
 if __name__ == "__main__":

@@ -193,6 +193,10 @@ int zt_inflate_dev(zt_inflate_plan *plan, const void *d_in, size_t n, void *d_ou
  * window) seeded with seed + i.  d_out must be 4-byte aligned.  With a
  * null stream the call returns when the data is written. */
 int zt_synth_dev(int kind, uint32_t seed, void *d_out, size_t n, void *stream);
+/* The same corpus from piece `piece0` on: bytes [piece0 * 65536, piece0 *
+ * 65536 + n) of the whole corpus (one rank's shard of a sharded buffer,
+ * config C3), so every rank generates exactly its slice. */
+int zt_synth_dev_at(int kind, uint32_t seed, uint64_t piece0, void *d_out, size_t n, void *stream);
 /* Kernel-time accounting with HIP events on the launch stream: the deflate
  * match-finding kernel (the dominant one), the whole deflate kernel pipeline,
  * and the inflate decode kernel of the device paths. */

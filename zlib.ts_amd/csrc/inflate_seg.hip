@@ -197,8 +197,15 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
     j.stop_first = (uint32_t)i;  // sync[i] is the first sync point after start
     j.end = 0;
   }
+  // Every candidate sync point gets a token slot before the chain shows which
+  // are real block boundaries, so a stream whose stored data is full of the
+  // pattern (or whose tail holds further members) could ask for far more
+  // than its decode needs: past a budget tied to the input size, or when the
+  // slots cannot be allocated, the stream takes the one-wave path instead.
+  const size_t tok_bytes = (units * (size_t)kUnitTokCap + 256) * 4;  // + slack: chunked token reads
+  if (tok_bytes > 16 * (n - index) + (64u << 20)) FALLBACK("%zu sync candidates: token slots over budget\n", units);
   void *d_tok, *d_meta;
-  ZT_TRY(scratch(c, 4, (units * (size_t)kUnitTokCap + 256) * 4, &d_tok));  // + slack: chunked token reads
+  if (scratch(c, 4, tok_bytes, &d_tok) != ZT_OK) FALLBACK("token slots (%zu B) not allocated\n", tok_bytes);
   const size_t stops_bytes = align256(sync.size() * 8);
   const size_t jobs_bytes = align256(units * sizeof(TokJob));
   const size_t res_bytes = align256(units * sizeof(TokResult));

@@ -33,10 +33,12 @@ struct WordOut {
   }
 };
 
-__global__ __launch_bounds__(64) void synth_kernel(int kind, uint32_t seed, uint8_t *out, uint64_t n) {
-  const uint64_t piece = (uint64_t)blockIdx.x * 64 + threadIdx.x;
-  const uint64_t lo = piece * kPieceBytes;
+__global__ __launch_bounds__(64) void synth_kernel(int kind, uint32_t seed, uint8_t *out, uint64_t n,
+                                                  uint64_t piece0) {
+  const uint64_t lpiece = (uint64_t)blockIdx.x * 64 + threadIdx.x;  // piece of this call's buffer
+  const uint64_t lo = lpiece * kPieceBytes;
   if (lo >= n) return;
+  const uint64_t piece = piece0 + lpiece;  // piece of the whole (sharded) corpus
   const uint32_t len = (uint32_t)((n - lo) < kPieceBytes ? (n - lo) : kPieceBytes);
   int k = kind;
   if (kind == 3) {
@@ -85,7 +87,7 @@ __global__ __launch_bounds__(64) void synth_kernel(int kind, uint32_t seed, uint
 
 using namespace zt;
 
-extern "C" int zt_synth_dev(int kind, uint32_t seed, void *d_out, size_t n, void *stream) {
+extern "C" int zt_synth_dev_at(int kind, uint32_t seed, uint64_t piece0, void *d_out, size_t n, void *stream) {
   if (kind < 0 || kind > 3) return set_error(ZT_E_ARG, "unknown generator");
   if (n == 0) return ZT_OK;
   if (!d_out) return set_error(ZT_E_ARG, "null output");
@@ -95,8 +97,12 @@ extern "C" int zt_synth_dev(int kind, uint32_t seed, void *d_out, size_t n, void
   std::lock_guard<std::recursive_mutex> ctx_lock(c->mu);
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   const uint64_t pieces = (n + kPieceBytes - 1) / kPieceBytes;
-  synth_kernel<<<(unsigned)((pieces + 63) / 64), 64, 0, s>>>(kind, seed, static_cast<uint8_t *>(d_out), n);
+  synth_kernel<<<(unsigned)((pieces + 63) / 64), 64, 0, s>>>(kind, seed, static_cast<uint8_t *>(d_out), n, piece0);
   ZT_HIP(hipGetLastError());
   if (!stream) ZT_HIP(hipStreamSynchronize(s));  // library stream: complete before returning
   return ZT_OK;
+}
+
+extern "C" int zt_synth_dev(int kind, uint32_t seed, void *d_out, size_t n, void *stream) {
+  return zt_synth_dev_at(kind, seed, 0, d_out, n, stream);
 }

@@ -5,7 +5,8 @@ The buffer is split into contiguous shards aligned to deflate's 1 MiB segment
 and final = (last rank), so the shards are independent segments and their
 streams concatenate, in rank order, into one valid raw DEFLATE stream whose
 segment markers let inflate run segment-parallel.  There is no collective on
-the data path; only timing uses a max-reduction.
+the data path; only timing uses a max-reduction (and the ratio a sum), over
+gloo on the host.
 """
 SEGMENT = 1 << 20
 
@@ -28,3 +29,14 @@ def max_over_ranks(value, dist=None, device="cpu"):
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def sum_over_ranks(value, dist=None):
+    """Sum of an integer over all ranks (total compressed bytes)."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return int(value)
+    import torch
+
+    t = torch.tensor([int(value)], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return int(t.item())

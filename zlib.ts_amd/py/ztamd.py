@@ -99,6 +99,7 @@ def _load():
         "zt_inflate_plan_destroy": ([vp], None),
         "zt_inflate_dev": ([vp, vp, sz, vp, sz, P(sz), P(sz), vp], ctypes.c_int),
         "zt_synth_dev": ([ctypes.c_int, u32, vp, sz, vp], ctypes.c_int),
+        "zt_synth_dev_at": ([ctypes.c_int, u32, ctypes.c_uint64, vp, sz, vp], ctypes.c_int),
         "zt_timing_enable": ([ctypes.c_int], ctypes.c_int),
         "zt_timing_read": ([P(KernelTimes)], ctypes.c_int),
     }
@@ -120,7 +121,7 @@ SYMBOLS = [
     "zt_deflate_raw_batch", "zt_gzip_compress", "zt_gunzip", "zt_zlib_compress", "zt_zlib_decompress",
     "zt_dev_checksums", "zt_deflate_plan_create", "zt_deflate_plan_destroy",
     "zt_deflate_bound", "zt_deflate_dev", "zt_inflate_plan_create", "zt_inflate_plan_destroy", "zt_inflate_dev",
-    "zt_synth_dev", "zt_timing_enable", "zt_timing_read",
+    "zt_synth_dev", "zt_synth_dev_at", "zt_timing_enable", "zt_timing_read",
 ]
 
 
@@ -355,6 +356,14 @@ def synth_dev(kind, seed, ptr, n, stream=None):
     """Fill device memory with a synthetic corpus (64 KiB piece i = generator
     seeded with seed + i)."""
     _check(lib.zt_synth_dev(GEN_KINDS.get(kind, kind), seed, ptr, n, stream))
+
+
+def synth_dev_at(kind, seed, offset, ptr, n, stream=None):
+    """Bytes [offset, offset + n) of the corpus synth_dev would write from 0
+    (offset a multiple of 64 KiB): one rank's shard of a sharded buffer."""
+    if offset % 65536:
+        raise ValueError("offset must be a multiple of 64 KiB")
+    _check(lib.zt_synth_dev_at(GEN_KINDS.get(kind, kind), seed, offset // 65536, ptr, n, stream))
 
 
 def timing_enable(on=True):
