@@ -1,33 +1,36 @@
 // deflate.hip -- raw DEFLATE (RFC 1951) encoder on the GPU.
 // Replaces src/LZ77.ts, src/RawDeflate.ts, src/Heap.ts and src/Bitstream.ts.
 //
-// Four kernels over device memory, each shaped for the phase it runs:
+// Kernels over device memory, each shaped for the phase it runs:
 //
-//   1. match_kernel -- one 1024-thread workgroup per super-chunk (K
+//   1. match_kernel -- one 1024-thread workgroup per super-chunk (4
 //      consecutive 32 KiB blocks; a 1 MiB segment starts without history,
-//      later super-chunks index the 32 KiB before them first).  4 KiB
-//      sub-chunks stream through a 36 KiB LDS ring; hash chains (13-bit hash
-//      of the first 3 or 4 bytes, u16 relative links, u32 absolute heads) are
-//      built lane-parallel (64-position steps: in-step predecessors by ballot
-//      peer masks, then one wave links the step leaders to the head table),
-//      and every position searches its chain (4 positions per thread, newest
-//      first, depth/nice limited, a long match carried to the next positions
-//      without a search).  The longest match of every position goes to HBM:
-//      res[i] = len << 16 | dist.  This is the LDS-bound kernel (one workgroup
-//      per CU); everything serial per block is moved out of it.
-//   2. block_kernel -- one wavefront per 32 KiB block (small LDS, many waves
-//      per CU, so per-block serial latency overlaps across blocks): greedy /
-//      one-step-lazy parse by pointer doubling over res (next(p) is a function
-//      of p; 6 bpermute rounds per 64-position window), tokens written over
-//      res in place, histograms, length-limited Huffman codes (bitonic sort +
-//      Moffat-Katajainen + JPEG-style limiting), the RLE'd code-length header
-//      written to the block's slot, and the smallest of stored / fixed /
-//      dynamic chosen.
-//   3. encode_kernel -- 256 threads per block: prefix sum of per-thread bit
-//      counts, interior words stored directly, boundary words merged by their
-//      first-touching thread; every block ends byte-aligned with an empty
-//      stored block (00 00 FF FF) so blocks concatenate bytewise.
-//   4. scan_sizes + gather_blocks -- exclusive scan of block sizes and a
+//      later super-chunks index the 28 KiB before them first).  4 KiB
+//      sub-chunks stream through a 32 KiB LDS ring (28 608-byte window).
+//      Wave 0 links 8-byte-key hash chains (u32 heads, u16 relative links)
+//      and wave 1 a 4-byte-key table (the newest earlier position per
+//      bucket), each by lane-ordered LDS exchanges head[h] <-> p, 64
+//      positions per exchange, publishing their progress; all waves search
+//      256-position super-steps as soon as they are linked: per thread 4
+//      positions, two chain walks interleaved (two LDS loads per hop: the
+//      link and one filter word), candidates measured against 16 bytes held
+//      in registers; matches shorter than the key come from near probes
+//      (distances 1..16, register window) and the 4-byte table.  The
+//      longest match of every position goes to HBM: res[i] = len << 16 |
+//      dist.
+//   2. price_kernel + optparse_kernel -- one wave per 32 KiB block: bit
+//      prices from the greedy parse of the block's first quarter, then a
+//      backward shortest-path DP over every position (cut lengths 3..16 and
+//      the full match), choices written over res.
+//   3. block_kernel -- one wave per block: parse of the DP's choices
+//      (LDS-DMA staged, pointer doubling), histograms, length-limited
+//      Huffman lengths by wave-parallel package-merge, canonical codes, the
+//      RLE'd code-length header, and the smallest of stored / fixed /
+//      dynamic.
+//   4. encode_kernel -- 256 threads per block: prefix sum of per-thread bit
+//      counts, word-parallel packing; every block ends byte-aligned with an
+//      empty stored block (00 00 FF FF) so blocks concatenate bytewise.
+//   5. scan_sizes + gather_blocks -- exclusive scan of block sizes and a
 //      byte-exact gather into the output stream; 1 MiB segment boundaries
 //      get a restart marker (two empty stored blocks) for segment-parallel
 //      inflate (inflate_seg.hip).
@@ -56,9 +59,20 @@ constexpr int DF_BLOCK = ZT_DF_BLOCK;
 constexpr int DF_SUB = 4096;
 constexpr int DF_RING = 32768;  // power of two: ring index = rel & (DF_RING - 1)
 constexpr int DF_SLOT = DF_BLOCK + DF_BLOCK / 8 + 1024;  // per-block slot: fits a forced fixed-code block
-// hash buckets: 2^14 minus 32 (the u32 head table leaves room in the 160 KiB
-// of LDS for the ring's wrap mirror and the work counters)
-constexpr uint32_t DF_HSIZE = (1u << 14) - 32;
+// hash buckets of the 8-byte-key chains (u32 heads) and of the 4-byte-key
+// table (u32 heads, no chains): the sizes fill the 160 KiB of LDS next to the
+// ring, the chain links and the sub-chunk's 4-byte links
+#ifndef ZT_DF_HSIZE
+#define ZT_DF_HSIZE 12240
+#endif
+#ifndef ZT_DF_H4SIZE
+#define ZT_DF_H4SIZE 2048
+#endif
+#ifndef ZT_DF_P4FAR
+#define ZT_DF_P4FAR 1024  // 4-byte (not longer) matches from the 4-byte-key table reach at most this far
+#endif
+constexpr uint32_t DF_HSIZE = ZT_DF_HSIZE;
+constexpr uint32_t DF_H4SIZE = ZT_DF_H4SIZE;
 constexpr int DF_THREADS = 1024;
 // the ring holds [p1 - DF_RING, p1) while sub-chunk [p0, p1) is searched;
 // a super-chunk loads DF_HIST bytes of history first (whole sub-chunks)
@@ -142,8 +156,12 @@ struct MatchShared {
   uint32_t ring[DF_RING / 4 + 16];  // data ring + 64-byte mirror of its start
   uint16_t prev[DF_RING];           // relative chain links (0 = none)
   uint32_t head[DF_HSIZE];          // newest position (rel) per hash bucket
-  uint32_t dummy[2];                // exchange / link target of lanes past the end (branch-free chain_link)
+  uint32_t head4[DF_H4SIZE];        // newest position (rel) per 4-byte-key bucket
+  uint16_t link4[DF_SUB];           // position p of the sub-chunk: distance to the newest earlier
+                                    // position of its 4-byte-key bucket (0 = none), at p % DF_SUB
+  uint32_t dummy[4];                // exchange / link targets of lanes past the end (branch-free chain_link)
   uint32_t linked;                  // positions below are linked (chain_link -> searching waves)
+  uint32_t linked4;                 // positions below have their 4-byte links
   uint32_t work;                    // next super-step of 256 positions to search
 };
 
@@ -173,6 +191,9 @@ __device__ __forceinline__ uint32_t key_hash(const MatchShared *s, uint32_t p, K
   const uint32_t v = (ld32(s, p) & k.kmask) ^ ((ld32(s, p + 4) & k.kmask2) * 0x2545F491u);
   return __umulhi(v * 0x9E3779B1u, DF_HSIZE);
 }
+__device__ __forceinline__ uint32_t key4_hash(const MatchShared *s, uint32_t p) {
+  return __umulhi(ld32(s, p) * 0x9E3779B1u, DF_H4SIZE);
+}
 
 // bytes [rel0, rel0 + len) of the super-chunk into the ring (len <= DF_SUB, rel0 % DF_SUB == 0)
 __device__ void load_sub(MatchShared *s, const uint8_t *g, uint32_t rel0, uint32_t len) {
@@ -200,8 +221,11 @@ __device__ void load_sub(MatchShared *s, const uint8_t *g, uint32_t rel0, uint32
 // earlier position of its bucket -- in its step or before -- and the head
 // ends at the step's last one.  Exchanges of later steps are issued without
 // waiting for earlier results (the wave's LDS operations stay in order); the
-// progress is published in s->linked for the searching waves (match_kernel).
+// progress is published for the searching waves (match_kernel).  T = 0: the
+// 8-byte-key chains (head -> prev, s->linked); T = 1, by a second wave at the
+// same time: the 4-byte-key table (head4 -> link4, s->linked4).
 constexpr int CL_U = 8;  // steps per group: hashes, then exchanges, then links
+template <int T>
 __device__ void chain_link(MatchShared *s, uint32_t lo, uint32_t hi, Key key) {
   const int lane = threadIdx.x & 63;
   const uint32_t nsteps = (hi - lo + 63) / 64;
@@ -210,7 +234,7 @@ __device__ void chain_link(MatchShared *s, uint32_t lo, uint32_t hi, Key key) {
 #pragma unroll
     for (int j = 0; j < CL_U; ++j) {
       const uint32_t p = lo + (sb + j) * 64 + lane;
-      h[j] = key_hash(s, p < hi ? p : lo, key);
+      h[j] = T == 0 ? key_hash(s, p < hi ? p : lo, key) : key4_hash(s, p < hi ? p : lo);
     }
   };
   hashes(0, hq);
@@ -221,7 +245,7 @@ __device__ void chain_link(MatchShared *s, uint32_t lo, uint32_t hi, Key key) {
 #pragma unroll
     for (int j = 0; j < CL_U; ++j) {
       const uint32_t p = lo + (sb + j) * 64 + lane;
-      uint32_t *hp = p < hi ? &s->head[hq[j]] : &s->dummy[0];
+      uint32_t *hp = p < hi ? (T == 0 ? &s->head[hq[j]] : &s->head4[hq[j]]) : &s->dummy[T];
       old[j] = atomicExch(hp, p);
     }
     hashes(sb + CL_U, hq);
@@ -229,12 +253,14 @@ __device__ void chain_link(MatchShared *s, uint32_t lo, uint32_t hi, Key key) {
     for (int j = 0; j < CL_U; ++j) {
       const uint32_t p = lo + (sb + j) * 64 + lane;
       const uint32_t d = p - old[j];
-      uint16_t *pp = p < hi ? &s->prev[ridx(p)] : reinterpret_cast<uint16_t *>(&s->dummy[1]);
+      uint16_t *pp = p < hi ? (T == 0 ? &s->prev[ridx(p)] : &s->link4[p & (DF_SUB - 1)])
+                            : reinterpret_cast<uint16_t *>(&s->dummy[2 + T]);
       *pp = (uint16_t)(d <= (uint32_t)DF_MAXDIST ? d : 0u);
     }
     const uint32_t done = lo + (sb + CL_U) * 64;
     if (lane == 0)
-      __hip_atomic_store(&s->linked, done < hi ? done : hi, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_store(T == 0 ? &s->linked : &s->linked4, done < hi ? done : hi, __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_WORKGROUP);
   }
 }
 
@@ -417,13 +443,38 @@ __device__ __forceinline__ void walk_pair_step(Walk &a, Walk &b, const MatchShar
   if (cb) walk_extend(b, s, P, qb);
 }
 
-// finish position pb + K: near probes when the chain found nothing long
+// finish position pb + K when the chain found nothing of the key's length:
+// the near probes, then the newest earlier position with the same 4 bytes
+// (the 4-byte-key table; the chains' 8-byte keys miss the 4..7-byte matches
+// that make up much of source text)
 template <int K>
-__device__ __forceinline__ uint32_t walk_finish(const Walk &w, const DeflateParams &P, const uint32_t (&win)[9],
-                                                uint32_t near, uint32_t &carry_len, uint32_t &carry_dist) {
+__device__ __forceinline__ uint32_t walk_finish(const Walk &w, const MatchShared *s, const DeflateParams &P,
+                                                const uint32_t (&win)[9], uint32_t near, uint32_t &carry_len,
+                                                uint32_t &carry_dist) {
   uint32_t best_len = w.best_len, best_dist = w.best_dist;
-  if (near == 0 && w.max_len >= 3 && best_len < (uint32_t)P.klen)
+  // a far 3-byte match (carried from the previous position) is dropped in
+  // the end: it must not hide a near one
+  if (best_len == 3 && best_dist > (uint32_t)P.too_far) best_len = 0;
+  const bool short_ = best_len < (uint32_t)P.klen;
+  if (near == 0 && w.max_len >= 3 && short_)
     near_probe<K, 1>(win, w.cur, w.cur2, w.p, w.max_len, P.probe, best_len, best_dist);
+#ifndef ZT_DF_NOP4
+  if (w.max_len >= 4 && short_) {
+    const uint32_t d4 = s->link4[w.p & (DF_SUB - 1)];
+    uint32_t qw[2];
+    ld_run<2>(s, w.p - d4, qw);
+    const uint32_t x0 = qw[0] ^ w.cur, x1 = qw[1] ^ w.cur2;
+    uint32_t len = x0 ? 0u : 4 + min((uint32_t)(__ffs(x1) - 1) >> 3, 4u);
+    len = len < w.max_len ? len : w.max_len;
+    // a far match must be longer by two bytes than a near one to replace it
+    // (its distance code costs more than the byte it gains)
+    const uint32_t need = best_len + (best_len >= 3 && d4 > (uint32_t)P.too_far ? 2u : 1u);
+    if (d4 != 0 && len >= 4 && len >= need && (len > 4 || d4 <= (uint32_t)ZT_DF_P4FAR)) {
+      best_len = len;
+      best_dist = d4;
+    }
+  }
+#endif
   carry_len = best_len;
   carry_dist = best_dist;
   if (best_len == 3 && best_dist > (uint32_t)P.too_far) best_len = 0;
@@ -448,13 +499,13 @@ __device__ void search_quad(const MatchShared *s, const DeflateParams &P, uint32
   walk_init(wa, s, P, pb, p1, win32<16>(w), win32<20>(w), win32<24>(w), win32<28>(w), 0, 0);
   walk_init(wb, s, P, pb + 2, p1, win32<18>(w), win32<22>(w), win32<26>(w), win32<30>(w), 0, 0);
   while (wa.active || wb.active) walk_pair_step(wa, wb, s, P);
-  out[0] = walk_finish<0>(wa, P, w, nr0, c0l, c0d);
-  out[2] = walk_finish<2>(wb, P, w, nr2, c2l, c2d);
+  out[0] = walk_finish<0>(wa, s, P, w, nr0, c0l, c0d);
+  out[2] = walk_finish<2>(wb, s, P, w, nr2, c2l, c2d);
   walk_init(wa, s, P, pb + 1, p1, win32<17>(w), win32<21>(w), win32<25>(w), win32<29>(w), c0l, c0d);
   walk_init(wb, s, P, pb + 3, p1, win32<19>(w), win32<23>(w), win32<27>(w), win32<31>(w), c2l, c2d);
   while (wa.active || wb.active) walk_pair_step(wa, wb, s, P);
-  out[1] = walk_finish<1>(wa, P, w, nr1, cl, cd);
-  out[3] = walk_finish<3>(wb, P, w, nr3, cl, cd);
+  out[1] = walk_finish<1>(wa, s, P, w, nr1, cl, cd);
+  out[3] = walk_finish<3>(wb, s, P, w, nr3, cl, cd);
   if (pb + 4 <= p1) {
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     u32x4 v = {out[0], out[1], out[2], out[3]};
@@ -488,6 +539,7 @@ __global__ __launch_bounds__(DF_THREADS) void match_kernel(DeflateParams P) {
   const uint32_t kext = (uint32_t)P.klen - 1;  // a key at p needs bytes up to p + kext
 
   for (uint32_t i = t; i < DF_HSIZE; i += DF_THREADS) s.head[i] = kNoHead;
+  for (uint32_t i = t; i < DF_H4SIZE; i += DF_THREADS) s.head4[i] = kNoHead;
   __syncthreads();
   uint32_t inserted = 0;  // positions [0, inserted) are in the chains
   if (re > 0) load_sub(&s, g, 0, re < DF_SUB ? re : DF_SUB);
@@ -502,6 +554,7 @@ __global__ __launch_bounds__(DF_THREADS) void match_kernel(DeflateParams P) {
     const bool link = ih > inserted;
     if (t == 0) {
       s.linked = link ? inserted : ih;
+      s.linked4 = link ? inserted : ih;
       s.work = 0;
     }
     // the next sub-chunk is fetched while this one is searched
@@ -511,10 +564,12 @@ __global__ __launch_bounds__(DF_THREADS) void match_kernel(DeflateParams P) {
     if (fast) nv = reinterpret_cast<const uint32_t *>(g + n0)[t];
     lds_barrier();
     DF_T(t1);
-    // wave 0 links the chains step by step; every wave (wave 0 once done)
-    // takes super-steps of 256 positions in order and searches them as soon
-    // as their links are final (positions only read links of older ones)
-    if (t < 64 && link) chain_link(&s, inserted, ih, key);
+    // wave 0 links the 8-byte-key chains and wave 1 the 4-byte-key table,
+    // step by step; every wave (waves 0 and 1 once done) takes super-steps of
+    // 256 positions in order and searches them as soon as their links are
+    // final (positions only read links of older ones)
+    if (t < 64 && link) chain_link<0>(&s, inserted, ih, key);
+    if (t >= 64 && t < 128 && link) chain_link<1>(&s, inserted, ih, key);
 #ifdef ZT_DF_TIME
     uint64_t tl;
     DF_T(tl);
@@ -530,7 +585,8 @@ __global__ __launch_bounds__(DF_THREADS) void match_kernel(DeflateParams P) {
         ss = (uint32_t)__shfl((int)ss, 0, 64);
         if (ss >= nss) break;
         const uint32_t need = (p0 + 256 * (ss + 1)) < ih ? (p0 + 256 * (ss + 1)) : ih;
-        while (__hip_atomic_load(&s.linked, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
+        while (min(__hip_atomic_load(&s.linked, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP),
+                   __hip_atomic_load(&s.linked4, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) < need)
           __builtin_amdgcn_s_sleep(1);
         search_quad(&s, P, p0 + 256 * ss + 4 * (t & 63), p0, p1, key, res_out);
       }
