@@ -71,7 +71,7 @@ int get_ctx(DeviceCtx **out) {
     hipDeviceProp_t prop;
     ZT_HIP(hipGetDeviceProperties(&prop, g_dev));
     c->num_cu = prop.multiProcessorCount;
-    uint32_t bt[256], nib[256], x2n[32];
+    uint32_t bt[256], nib[ZT_CRC_NIB_N], x2n[32];
     crc_host_tables(bt, nib, x2n);
     ZT_HIP(hipMalloc(&c->d_crc_nib, sizeof nib));
     ZT_HIP(hipMalloc(&c->d_crc_x2n, sizeof x2n));

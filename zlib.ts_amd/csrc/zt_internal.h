@@ -39,7 +39,7 @@ struct DeviceCtx {
   hipStream_t stream = nullptr;
   int num_cu = 0;
   // checksum constants (uploaded once)
-  uint32_t *d_crc_nib = nullptr;    // 16 x 16 nibble tables (slice-by-8)
+  uint32_t *d_crc_nib = nullptr;    // nibble tables (ZT_CRC_NIB_N entries)
   uint32_t *d_crc_x2n = nullptr;    // x^(2^k) mod P, k = 0..31
   uint32_t *d_crc_shift = nullptr;  // checksum.hip merge constants (crc_shift_tables)
   // scratch
@@ -121,12 +121,17 @@ __host__ __device__ __forceinline__ uint32_t dist_extra(uint32_t ds) { return ds
 typedef __attribute__((address_space(1))) const uint8_t g_u8;
 typedef __attribute__((address_space(1))) const uint32_t g_u32;
 
-void crc_host_tables(uint32_t byte_table[256], uint32_t nib[256], uint32_t x2n[32]);
-// x^(8 L) mod P for the checksum kernels: [0, 256] fixed slice/segment merge
-// shifts, then ZT_CRC_DIGITS tables of 64 entries x^(8 v 64^d)
+// nibble tables: 16 x 16 for slice-by-8, then 8 x 16 for the multiplication
+// by x^(8 * 1024) (checksum.hip's coalesced lane streams)
+#define ZT_CRC_NIB_N 384
+void crc_host_tables(uint32_t byte_table[256], uint32_t nib[ZT_CRC_NIB_N], uint32_t x2n[32]);
+// x^(8 L) mod P for the checksum kernels: [0, 264) unused, then
+// ZT_CRC_DIGITS tables of 64 entries x^(8 v 64^d), then per thread of a whole
+// segment the shift of its lane stream to the segment end
 #define ZT_CRC_DIGITS 6
 #define ZT_CRC_DIG_OFF 264
-#define ZT_CRC_SHIFT_N (ZT_CRC_DIG_OFF + 64 * ZT_CRC_DIGITS)
+#define ZT_CRC_LANE_OFF (ZT_CRC_DIG_OFF + 64 * ZT_CRC_DIGITS)
+#define ZT_CRC_SHIFT_N (ZT_CRC_LANE_OFF + 512)
 void crc_shift_tables(const uint32_t x2n[32], uint32_t shift[ZT_CRC_SHIFT_N]);
 
 // ---- launchers (device-resident) ------------------------------------------------
