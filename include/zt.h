@@ -51,6 +51,10 @@ extern "C" {
 int zt_device_count(void);
 /* Select the device used by the calling thread (default 0). */
 int zt_set_device(int device);
+/* Devices the batch calls (zt_*_batch) split their buffers over: bit d =
+ * device d (config C4: one node's GPUs, no collective -- every buffer is
+ * independent).  0 restores the default: the calling thread's device. */
+int zt_set_devices(uint64_t mask);
 /* Text of the last error on this thread, formatted like the reference's
  * message (e.g. "invalid code length: 9"). */
 const char *zt_last_error_message(void);
@@ -126,6 +130,20 @@ typedef struct {
  * header + raw DEFLATE + CRC-32 + ISIZE.  *crc_out (may be NULL) = GZip.crc32. */
 int zt_gzip_compress(const uint8_t *in, size_t n, const zt_gzip_opts *opts, uint8_t **out, size_t *out_len,
                      uint32_t *crc_out);
+
+/* Batch GZip (config C4): `count` independent members, each as
+ * zt_gzip_compress makes it (the same opts for all), in one pipeline per
+ * device: the buffers are packed at 32 KiB boundaries and uploaded once, the
+ * batch deflate pipeline and the batched CRC-32 kernels read the same device
+ * bytes, and the devices of zt_set_devices share the batch (largest buffers
+ * first onto the least loaded device).  out[i] is malloc'd (zt_free).
+ * Replaces a loop of new GZip(in[i], opts).compress()  src/GZip.ts:96-194. */
+int zt_gzip_compress_batch(const uint8_t *const *in, const size_t *n, size_t count, const zt_gzip_opts *opts,
+                           uint8_t **out, size_t *out_len, int *status);
+/* The same for zlib streams: a loop of new Deflate(in[i], opts).compress()
+ * src/Deflate.ts:60-99 (CMF/FLG, raw DEFLATE, Adler-32). */
+int zt_zlib_compress_batch(const uint8_t *const *in, const size_t *n, size_t count, const zt_deflate_opts *opts,
+                           uint8_t **out, size_t *out_len, int *status);
 
 /* One decoded member (GUnzipMember, src/GUnzip.ts:66-175).  Offsets index the
  * input buffer (name, comment) or the concatenated output (data). */
@@ -209,6 +227,11 @@ typedef struct {
   uint64_t deflate_pipelines;
   double inflate_tok_ms; /* two-phase inflate: phase A (tokenize_kernel) alone */
   uint64_t inflate_toks;
+  /* streams inflated per path (counted whether timing is on or not):
+   * [0] sync-point two-phase, [1] general speculative (streams without sync
+   * points), [2] one wave per stream */
+  uint64_t inflate_paths[3];
+  uint64_t general_passes; /* decode passes of the general path (1 = no redo) */
 } zt_kernel_times;
 int zt_timing_enable(int on); /* resets the counters */
 int zt_timing_read(zt_kernel_times *out);

@@ -1,0 +1,280 @@
+// batch_api.cpp -- many independent buffers per call (configs C4 and C2's
+// producer side; include/zt.h): zt_gzip_compress_batch, zt_zlib_compress_batch
+// and zt_deflate_raw_batch.
+//
+// Per device, one pipeline for the whole share: the buffers are packed into
+// pinned staging at 32 KiB boundaries and uploaded with one copy; the batch
+// deflate pipeline (deflate.hip, one match workgroup per block so no history
+// crosses buffers) runs on the main stream while the batched CRC-32 /
+// Adler-32 kernels read the same device bytes on the second stream; one copy
+// brings every stream back.  With zt_set_devices(mask) the buffers are split
+// over the devices by longest-processing-time (largest first onto the least
+// loaded device) and each device's share runs on its own host thread.
+// Replaces a loop of new GZip(input).compress() (src/GZip.ts:96-194),
+// new Deflate(input).compress() (src/Deflate.ts:60-99) and
+// new RawDeflate(input).compress() (src/RawDeflate.ts:87-114).
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "zt_internal.h"
+
+namespace zt {
+
+namespace {
+
+constexpr uint64_t kBlk = 32768;
+
+size_t round_blk(size_t n) { return (n + kBlk - 1) / kBlk * kBlk; }
+
+// fills out[i] (malloc'd: prefix | stream | trailer) for item i
+struct Framing {
+  enum Kind { RAW, GZIP, ZLIB } kind;
+  std::vector<uint8_t> prefix;
+  size_t trailer;
+};
+
+int frame_item(const Framing &fr, size_t n_in, const uint8_t *body, size_t blen, uint32_t crc, uint32_t adler,
+               uint8_t **out, size_t *out_len) {
+  const size_t total = fr.prefix.size() + blen + fr.trailer;
+  uint8_t *h = (uint8_t *)malloc(total ? total : 1);
+  if (!h) return set_error(ZT_E_NOMEM, "host allocation failed");
+  if (!fr.prefix.empty()) memcpy(h, fr.prefix.data(), fr.prefix.size());
+  if (blen) memcpy(h + fr.prefix.size(), body, blen);
+  uint8_t *t = h + fr.prefix.size() + blen;
+  if (fr.kind == Framing::GZIP) {  // CRC-32, ISIZE (src/GZip.ts:179-185)
+    for (int k = 0; k < 4; ++k) t[k] = (crc >> (8 * k)) & 0xFF;
+    for (int k = 0; k < 4; ++k) t[4 + k] = ((uint32_t)n_in >> (8 * k)) & 0xFF;
+  } else if (fr.kind == Framing::ZLIB) {  // Adler-32 big-endian (src/Deflate.ts:95)
+    for (int k = 0; k < 4; ++k) t[k] = (adler >> (24 - 8 * k)) & 0xFF;
+  }
+  *out = h;
+  *out_len = total;
+  return ZT_OK;
+}
+
+// one device's share: items `ids` of the batch
+int batch_on_device(int dev, const uint8_t *const *in, const size_t *n, const std::vector<size_t> &ids, int ct,
+                    int lv, const Framing &fr, uint8_t **out, size_t *out_len, std::string *err) {
+  auto fail = [&](int rc) {
+    *err = zt_last_error_message();
+    return rc;
+  };
+  if (zt_set_device(dev)) return fail(ZT_E_NO_DEVICE);
+  DeviceCtx *c;
+  if (int rc = get_ctx(&c)) return fail(rc);
+  std::lock_guard<std::recursive_mutex> ctx_lock(c->mu);
+  const bool sums = fr.kind != Framing::RAW;
+  // empty inputs: a final empty stored block, as the one-buffer calls write
+  // (deflate.hip) -- no device work
+  std::vector<size_t> work;
+  for (size_t i : ids) {
+    if (n[i] == 0) {
+      static const uint8_t empty_stored[5] = {0x01, 0x00, 0x00, 0xFF, 0xFF};
+      const int rc = frame_item(fr, 0, empty_stored, 5, 0, 1, &out[i], &out_len[i]);
+      if (rc) return fail(rc);
+    } else {
+      work.push_back(i);
+    }
+  }
+  if (work.empty()) return ZT_OK;
+  const size_t m = work.size();
+  std::vector<uint64_t> off(m), len(m);
+  uint64_t padded = 0, in_bytes = 0;
+  for (size_t k = 0; k < m; ++k) {
+    off[k] = padded;
+    len[k] = n[work[k]];
+    padded += round_blk(len[k]);
+    in_bytes += len[k];
+  }
+  void *d_in, *h_stage;
+  if (int rc = scratch(c, 0, padded + 64, &d_in)) return fail(rc);
+  if (int rc = pinned(c, padded, &h_stage, 0)) return fail(rc);
+  uint8_t *stage = static_cast<uint8_t *>(h_stage);
+  parallel_copy(m, [&](size_t k) {
+    memcpy(stage + off[k], in[work[k]], len[k]);
+    memset(stage + off[k] + len[k], 0, round_blk(len[k]) - len[k]);
+  }, in_bytes);
+  ZT_HIP(hipMemcpyAsync(d_in, stage, padded, hipMemcpyHostToDevice, c->stream));
+  // checksums on the second stream, over the same device bytes
+  std::vector<uint32_t> hsums(2 * m, 0);
+  void *d_sums = nullptr;
+  struct AuxWait {
+    hipStream_t s;
+    ~AuxWait() { (void)hipStreamSynchronize(s); }
+  } aux_wait{c->aux};
+  if (sums) {
+    if (int rc = scratch(c, 18, 8 * m, &d_sums)) return fail(rc);
+    ZT_HIP(hipEventRecord(c->aux_ev, c->stream));
+    ZT_HIP(hipStreamWaitEvent(c->aux, c->aux_ev, 0));
+    if (int rc = checksums_batch_dev(c, (const uint8_t *)d_in, m, off.data(), len.data(), (uint32_t *)d_sums, c->aux))
+      return fail(rc);
+    ZT_HIP(hipMemcpyAsync(hsums.data(), d_sums, 8 * m, hipMemcpyDeviceToHost, c->aux));
+  }
+  std::vector<uint64_t> oo(m + 1, 0);
+  uint8_t *body_host = nullptr;
+  std::vector<uint8_t> stored_host;
+  if (ct == 0) {
+    // stored blocks of <= 65535 bytes (src/RawDeflate.ts:93-100,122-153): framing only
+    uint64_t tot = 0;
+    for (size_t k = 0; k < m; ++k) {
+      oo[k] = tot;
+      tot += len[k] + 5 * ((len[k] + 65534) / 65535);
+    }
+    oo[m] = tot;
+    stored_host.resize(tot);
+    for (size_t k = 0; k < m; ++k) {
+      uint8_t *o = stored_host.data() + oo[k];
+      const uint8_t *src = in[work[k]];
+      for (uint64_t p = 0; p < len[k]; p += 65535) {
+        const uint32_t l = (uint32_t)std::min<uint64_t>(65535, len[k] - p);
+        o[0] = p + l == len[k] ? 1 : 0;
+        o[1] = l & 0xFF;
+        o[2] = l >> 8;
+        o[3] = ~l & 0xFF;
+        o[4] = (~l >> 8) & 0xFF;
+        memcpy(o + 5, src + p, l);
+        o += 5 + l;
+      }
+    }
+    body_host = stored_host.data();
+  } else {
+    const size_t ob = padded + padded / 8 + 1024 * (padded / kBlk + 1) + 4096;
+    void *d_out, *d_scr;
+    if (int rc = scratch(c, 1, ob, &d_out)) return fail(rc);
+    const size_t ss = deflate_batch_scratch_bytes(c, padded);
+    if (int rc = scratch(c, 3, ss, &d_scr)) return fail(rc);
+    if (int rc = deflate_batch_dev_run(c, (const uint8_t *)d_in, m, off.data(), len.data(), ct, lv,
+                                       (uint8_t *)d_out, oo.data(), d_scr, ss, c->stream))
+      return fail(rc);
+    // the staged input has been consumed (the pipeline waited for its stream)
+    void *h_out;
+    if (int rc = pinned(c, oo[m], &h_out, 0)) return fail(rc);
+    ZT_HIP(hipMemcpyAsync(h_out, d_out, oo[m], hipMemcpyDeviceToHost, c->stream));
+    ZT_HIP(hipStreamSynchronize(c->stream));
+    body_host = static_cast<uint8_t *>(h_out);
+  }
+  ZT_HIP(hipStreamSynchronize(c->aux));
+  int first_rc = ZT_OK;
+  std::vector<int> rcs(m, ZT_OK);
+  parallel_copy(m, [&](size_t k) {
+    const size_t i = work[k];
+    rcs[k] = frame_item(fr, len[k], body_host + oo[k], oo[k + 1] - oo[k], hsums[2 * k], hsums[2 * k + 1], &out[i],
+                        &out_len[i]);
+  }, oo[m]);
+  for (int rc : rcs)
+    if (rc && !first_rc) first_rc = rc;
+  return first_rc ? fail(first_rc) : ZT_OK;
+}
+
+// split over the batch devices (LPT) and run every share on its own thread
+int run_batch(const uint8_t *const *in, const size_t *n, size_t count, int ct, int lv, const Framing &fr,
+              uint8_t **out, size_t *out_len, int *status) {
+  for (size_t i = 0; i < count; ++i) {
+    out[i] = nullptr;
+    out_len[i] = 0;
+    if (n[i] && !in[i]) return set_error(ZT_E_ARG, "null input");
+  }
+  const std::vector<int> devs = batch_devices();
+  const size_t nd = devs.size();
+  std::vector<std::vector<size_t>> share(nd);
+  if (nd == 1) {
+    share[0].resize(count);
+    for (size_t i = 0; i < count; ++i) share[0][i] = i;
+  } else {
+    std::vector<size_t> order(count);
+    for (size_t i = 0; i < count; ++i) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return n[a] > n[b]; });
+    std::vector<uint64_t> load(nd, 0);
+    for (size_t i : order) {
+      const size_t d = (size_t)(std::min_element(load.begin(), load.end()) - load.begin());
+      share[d].push_back(i);
+      load[d] += n[i] + 4096;  // + per-item cost
+    }
+    for (auto &v : share) std::sort(v.begin(), v.end());
+  }
+  std::vector<int> rc(nd, ZT_OK);
+  std::vector<std::string> err(nd);
+  const int caller_dev = current_device();
+  if (nd == 1) {
+    rc[0] = batch_on_device(devs[0], in, n, share[0], ct, lv, fr, out, out_len, &err[0]);
+    zt_set_device(caller_dev);
+  } else {
+    std::vector<std::thread> th;
+    for (size_t d = 0; d < nd; ++d)
+      th.emplace_back([&, d] { rc[d] = batch_on_device(devs[d], in, n, share[d], ct, lv, fr, out, out_len, &err[d]); });
+    for (auto &t : th) t.join();
+  }
+  int first = ZT_OK;
+  for (size_t d = 0; d < nd; ++d) {
+    for (size_t i : share[d]) status[i] = rc[d];
+    if (rc[d] && first == ZT_OK) {
+      first = rc[d];
+      set_error(rc[d], err[d]);
+    }
+  }
+  if (first) {
+    for (size_t i = 0; i < count; ++i) {
+      free(out[i]);
+      out[i] = nullptr;
+      out_len[i] = 0;
+    }
+  }
+  return first;
+}
+
+int resolve_opts(const zt_deflate_opts *o, int *ct, int *lv) {
+  int c = o ? o->compression_type : 2;
+  int l = o ? o->level : -1;
+  if (c < 0 || c > 2) return set_error(ZT_E_INVALID_COMPRESSION_TYPE, "invalid compression type");
+  if (l < 0 || l > 9) l = 6;
+  if (l == 0) c = 0;
+  if (o && o->lazy > 0 && l < 4) l = 4;
+  *ct = c;
+  *lv = l;
+  return ZT_OK;
+}
+
+}  // namespace
+}  // namespace zt
+
+using namespace zt;
+
+extern "C" {
+
+int zt_deflate_raw_batch(const uint8_t *const *in, const size_t *n, size_t count, const zt_deflate_opts *opts,
+                         uint8_t **out, size_t *out_len, int *status) {
+  if (count == 0) return ZT_OK;
+  if (!in || !n || !out || !out_len || !status) return set_error(ZT_E_ARG, "null argument");
+  int ct, lv;
+  ZT_TRY(resolve_opts(opts, &ct, &lv));
+  Framing fr{Framing::RAW, {}, 0};
+  return run_batch(in, n, count, ct, lv, fr, out, out_len, status);
+}
+
+int zt_gzip_compress_batch(const uint8_t *const *in, const size_t *n, size_t count, const zt_gzip_opts *opts,
+                           uint8_t **out, size_t *out_len, int *status) {
+  if (count == 0) return ZT_OK;
+  if (!in || !n || !out || !out_len || !status) return set_error(ZT_E_ARG, "null argument");
+  int ct, lv;
+  ZT_TRY(resolve_opts(opts ? &opts->deflate : nullptr, &ct, &lv));
+  Framing fr{Framing::GZIP, {}, 8};
+  gzip_header(opts, fr.prefix);
+  return run_batch(in, n, count, ct, lv, fr, out, out_len, status);
+}
+
+int zt_zlib_compress_batch(const uint8_t *const *in, const size_t *n, size_t count, const zt_deflate_opts *opts,
+                           uint8_t **out, size_t *out_len, int *status) {
+  if (count == 0) return ZT_OK;
+  if (!in || !n || !out || !out_len || !status) return set_error(ZT_E_ARG, "null argument");
+  int ct, lv;
+  ZT_TRY(resolve_opts(opts, &ct, &lv));
+  const uint32_t cmf = 0x78, flg0 = (uint32_t)(opts ? opts->compression_type : 2) << 6;
+  Framing fr{Framing::ZLIB, {(uint8_t)cmf, (uint8_t)(flg0 | (31 - ((cmf << 8) + flg0) % 31))}, 4};
+  return run_batch(in, n, count, ct, lv, fr, out, out_len, status);
+}
+
+}  // extern "C"

@@ -22,6 +22,8 @@
 //     sums (Adler) inside the workgroup, then one tiny kernel merges segments.
 //     Ragged first / last segments take a byte-wise per-thread-slice path.
 // Algorithmic bytes per unit: N input bytes read.
+#include <vector>
+
 #include "zt_internal.h"
 
 namespace zt {
@@ -41,6 +43,13 @@ constexpr int NIB_ENTRIES = ZT_CRC_NIB_N;            // (16 + 8) nibble position
 constexpr int ADV = 16;                              // first nibble table of x^(8*1024) * v
 constexpr int CK_WAVE_BYTES = 262144 / (CK_THREADS / 64);  // contiguous bytes per wave in a whole segment
 static_assert(CK_WAVE_BYTES * (CK_THREADS / 64) == (int)CK_SEG, "waves tile the segment");
+
+// batch checksums: segment k of the buffer at frame + off (off 16-byte aligned)
+struct CkJob {
+  uint64_t off;
+  uint64_t len;
+  uint64_t k;
+};
 
 struct SegResult {
   uint32_t crc;   // raw CRC register (init 0, no final xor) over the segment's bytes
@@ -120,12 +129,13 @@ __device__ inline uint32_t shift_bytes(const uint32_t *__restrict__ dig, const u
 }
 
 template <bool DO_CRC, bool DO_ADLER>
-__global__ __launch_bounds__(CK_THREADS) void checksum_segments(const uint8_t *__restrict__ frame, size_t lo,
-                                                                 size_t hi, size_t nseg,
+__global__ __launch_bounds__(CK_THREADS) void checksum_segments(const uint8_t *__restrict__ frame0, size_t lo0,
+                                                                 size_t hi0, size_t nseg,
                                                                  const uint32_t *__restrict__ nib_g,
                                                                  const uint32_t *__restrict__ x2n_g,
                                                                  const uint32_t *__restrict__ shift_g,
-                                                                 SegResult *__restrict__ out) {
+                                                                 SegResult *__restrict__ out,
+                                                                 const CkJob *__restrict__ jobs = nullptr) {
   // 32 KiB of replicated nibble tables + the combine scratch
   __shared__ uint32_t T[DO_CRC ? NIB_ENTRIES * 32 : 1];
   __shared__ uint32_t x2n[32];
@@ -148,7 +158,17 @@ __global__ __launch_bounds__(CK_THREADS) void checksum_segments(const uint8_t *_
   __syncthreads();
 
   for (size_t seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
-    const size_t seg_lo = seg * CK_SEG;
+    // one buffer, or (batch) segment k of buffer `jobs[seg]` (16-byte aligned)
+    const uint8_t *frame = frame0;
+    size_t lo = lo0, hi = hi0, kseg = seg;
+    if (jobs) {
+      const CkJob j = jobs[seg];
+      frame = frame0 + j.off;
+      lo = 0;
+      hi = j.len;
+      kseg = j.k;
+    }
+    const size_t seg_lo = kseg * CK_SEG;
     const size_t s_lo = seg_lo + (size_t)tid * CK_SLICE;
     const size_t v_lo = s_lo > lo ? s_lo : lo;                              // valid start
     const size_t v_hi = (s_lo + CK_SLICE) < hi ? (s_lo + CK_SLICE) : hi;    // valid end
@@ -369,6 +389,30 @@ __global__ __launch_bounds__(CF_THREADS) void checksum_finish(const SegResult *_
   }
 }
 
+// batch: one lane per buffer, its segments [first[i], first[i + 1]) merged
+__global__ __launch_bounds__(256) void checksum_batch_finish(const SegResult *__restrict__ segs,
+                                                             const uint32_t *__restrict__ first,
+                                                             const uint64_t *__restrict__ lens, uint32_t count,
+                                                             const uint32_t *__restrict__ x2n_g,
+                                                             const uint32_t *__restrict__ shift_g,
+                                                             uint32_t *__restrict__ result) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= count) return;
+  uint32_t raw = 0;
+  uint64_t t1 = 0, t2 = 0;
+  for (uint32_t k = first[i]; k < first[i + 1]; ++k) {
+    const SegResult r = segs[k];
+    raw ^= r.crc;
+    t1 += r.s1;
+    t2 += r.s2;
+  }
+  const uint64_t n = lens[i];
+  result[2 * i] = ~(shift_bytes(shift_g + ZT_CRC_DIG_OFF, x2n_g, n, 0xFFFFFFFFu) ^ raw);
+  const uint64_t f1 = (1 + t1 % 65521u) % 65521u;
+  const uint64_t f2 = ((n % 65521u) + t2 % 65521u) % 65521u;
+  result[2 * i + 1] = (uint32_t)((f2 << 16) | f1);
+}
+
 }  // namespace
 
 void crc_host_tables(uint32_t byte_table[256], uint32_t nib[ZT_CRC_NIB_N], uint32_t x2n[32]) {
@@ -407,6 +451,46 @@ void crc_shift_tables(const uint32_t x2n[32], uint32_t shift[ZT_CRC_SHIFT_N]) {
   // digit tables: x^(8 * v * 64^d)
   for (int d = 0; d < ZT_CRC_DIGITS; ++d)
     for (uint64_t v = 0; v < 64; ++v) shift[ZT_CRC_DIG_OFF + d * 64 + v] = x2nmodp(x2n, v << (6 * d), 3);
+}
+
+// CRC-32 and Adler-32 (initial values 0 and 1) of `count` buffers at
+// frame + off[i] (16-byte aligned) in one launch pair: d_result[2 i] = CRC,
+// d_result[2 i + 1] = Adler.  Empty buffers give 0 / 1.
+int checksums_batch_dev(DeviceCtx *c, const uint8_t *frame, size_t count, const uint64_t *off, const uint64_t *len,
+                        uint32_t *d_result, hipStream_t s) {
+  if (count == 0) return ZT_OK;
+  std::vector<CkJob> jobs;
+  std::vector<uint32_t> first(count + 1);
+  for (size_t i = 0; i < count; ++i) {
+    if (off[i] & 15) return set_error(ZT_E_ARG, "batch checksum buffers must be 16-byte aligned");
+    first[i] = (uint32_t)jobs.size();
+    const uint64_t ns = (len[i] + CK_SEG - 1) / CK_SEG;
+    for (uint64_t k = 0; k < ns; ++k) jobs.push_back(CkJob{off[i], len[i], k});
+  }
+  first[count] = (uint32_t)jobs.size();
+  const size_t nj = jobs.size();
+  const size_t jb = (nj * sizeof(CkJob) + 255) & ~size_t(255), fb = ((count + 1) * 4 + 255) & ~size_t(255);
+  const size_t lb = (count * 8 + 255) & ~size_t(255), sb = ((nj ? nj : 1) * sizeof(SegResult) + 255) & ~size_t(255);
+  void *buf;
+  ZT_TRY(scratch(c, 9, jb + fb + lb + sb, &buf));
+  uint8_t *b = static_cast<uint8_t *>(buf);
+  CkJob *d_jobs = reinterpret_cast<CkJob *>(b);
+  uint32_t *d_first = reinterpret_cast<uint32_t *>(b + jb);
+  uint64_t *d_len = reinterpret_cast<uint64_t *>(b + jb + fb);
+  SegResult *d_seg = reinterpret_cast<SegResult *>(b + jb + fb + lb);
+  // small tables: blocking copies (the kernels below stay asynchronous)
+  if (nj) ZT_HIP(hipMemcpy(d_jobs, jobs.data(), nj * sizeof(CkJob), hipMemcpyHostToDevice));
+  ZT_HIP(hipMemcpy(d_first, first.data(), (count + 1) * 4, hipMemcpyHostToDevice));
+  ZT_HIP(hipMemcpy(d_len, len, count * 8, hipMemcpyHostToDevice));
+  if (nj) {
+    checksum_segments<true, true><<<(unsigned)nj, CK_THREADS, 0, s>>>(frame, 0, 0, nj, c->d_crc_nib, c->d_crc_x2n,
+                                                                      c->d_crc_shift, d_seg, d_jobs);
+    ZT_HIP(hipGetLastError());
+  }
+  checksum_batch_finish<<<(unsigned)((count + 255) / 256), 256, 0, s>>>(d_seg, d_first, d_len, (uint32_t)count,
+                                                                        c->d_crc_x2n, c->d_crc_shift, d_result);
+  ZT_HIP(hipGetLastError());
+  return ZT_OK;
 }
 
 int checksums_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, bool do_crc, bool do_adler, uint32_t crc_in,

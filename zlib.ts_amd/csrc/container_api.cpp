@@ -117,18 +117,10 @@ struct Reader {
 std::string num(int v) { return v < 0 ? std::string("undefined") : std::to_string(v); }
 
 }  // namespace
-}  // namespace zt
 
-using namespace zt;
-
-extern "C" {
-
-int zt_gzip_compress(const uint8_t *in, size_t n, const zt_gzip_opts *opts, uint8_t **out, size_t *out_len,
-                     uint32_t *crc_out) {
-  if (!out || !out_len) return set_error(ZT_E_ARG, "null output");
-  if (n && !in) return set_error(ZT_E_ARG, "null input");
-  // header: src/GZip.ts:104-158
-  std::vector<uint8_t> hd = {0x1F, 0x8B, 8};
+// member header: src/GZip.ts:104-158
+void gzip_header(const zt_gzip_opts *opts, std::vector<uint8_t> &hd) {
+  hd = {0x1F, 0x8B, 8};
   uint8_t flg = 0;
   if (opts && opts->fname) flg |= 0x08;
   if (opts && opts->fcomment) flg |= 0x10;
@@ -151,6 +143,19 @@ int zt_gzip_compress(const uint8_t *in, size_t n, const zt_gzip_opts *opts, uint
     hd.push_back(c16 & 0xFF);
     hd.push_back(c16 >> 8);
   }
+}
+}  // namespace zt
+
+using namespace zt;
+
+extern "C" {
+
+int zt_gzip_compress(const uint8_t *in, size_t n, const zt_gzip_opts *opts, uint8_t **out, size_t *out_len,
+                     uint32_t *crc_out) {
+  if (!out || !out_len) return set_error(ZT_E_ARG, "null output");
+  if (n && !in) return set_error(ZT_E_ARG, "null input");
+  std::vector<uint8_t> hd;
+  gzip_header(opts, hd);
   uint8_t *buf;
   size_t slen;
   uint32_t crc;

@@ -36,6 +36,7 @@
 //      inflate (inflate_seg.hip).
 #include <cstdio>
 #include <cstdlib>
+#include <vector>
 
 #include "zt_internal.h"
 
@@ -105,6 +106,10 @@ struct DeflateParams {
   int probe;            // near distances 1..probe checked for matches shorter than klen
   int ctype;            // 1: fixed codes only; 2: best of dynamic/fixed/stored
   int opt;              // cost-based parse (optparse_kernel) between match and block kernels
+  // batch of independent streams (zt_deflate_batch_dev): stream f occupies
+  // whole blocks from a 32 KiB-aligned offset; per block the [start, end) of
+  // its stream (relative to halo = 0), or null for one stream of n bytes
+  const uint64_t *span;
   uint32_t *res;        // n: per-position match, then (in place) per-block tokens
   uint8_t *slots;       // nblocks x DF_SLOT
   uint32_t *slot_len;   // nblocks
@@ -125,6 +130,11 @@ struct BlockPlan {
 };
 
 namespace {
+
+// end of the stream block `blk` belongs to (relative to base + halo)
+__device__ __forceinline__ uint64_t stream_end(const DeflateParams &P, uint32_t blk) {
+  return P.span ? P.span[2 * (uint64_t)blk + 1] : P.end - P.halo;
+}
 
 __constant__ uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
@@ -521,18 +531,22 @@ __global__ __launch_bounds__(DF_THREADS) void match_kernel(DeflateParams P) {
   const uint32_t wg = blockIdx.x;
   const uint32_t b0 = wg * P.blocks_per_wg;
   const uint32_t b1 = (b0 + P.blocks_per_wg) < P.nblocks ? (b0 + P.blocks_per_wg) : P.nblocks;
+  // (batch: a workgroup's blocks belong to one stream, which starts at f_lo)
+  const uint64_t f_lo = P.span ? P.halo + P.span[2 * (uint64_t)b0] : 0;
+  const uint64_t f_end = P.span ? P.halo + P.span[2 * (uint64_t)b0 + 1] : P.end;
   const uint64_t s_lo = P.halo + (uint64_t)b0 * DF_BLOCK;
-  const uint64_t s_hi = (P.halo + (uint64_t)b1 * DF_BLOCK) < P.end ? (P.halo + (uint64_t)b1 * DF_BLOCK) : P.end;
+  const uint64_t s_hi = (P.halo + (uint64_t)b1 * DF_BLOCK) < f_end ? (P.halo + (uint64_t)b1 * DF_BLOCK) : f_end;
   // a segment start (restart point) sees no history: its matches stay inside
   // the segment, so inflate can decode segments independently
-  const bool restart = (b0 % P.restart) == 0 && (b0 > 0 || P.halo == 0);
+  const bool restart = P.span ? (((s_lo - f_lo) / DF_BLOCK) % P.restart) == 0
+                              : (b0 % P.restart) == 0 && (b0 > 0 || P.halo == 0);
   // history: whole sub-chunks, so that the searched range starts on a sub-chunk
   const uint64_t hmax = P.hist_max;
-  const uint64_t hist = restart ? 0 : (s_lo < hmax ? (s_lo & ~uint64_t(DF_SUB - 1)) : hmax);
+  const uint64_t hist = restart ? 0 : ((s_lo - f_lo) < hmax ? ((s_lo - f_lo) & ~uint64_t(DF_SUB - 1)) : hmax);
   const uint64_t h_lo = s_lo - hist;
   const uint8_t *g = P.base + h_lo;  // rel 0
   const uint32_t rs = (uint32_t)(s_lo - h_lo), re = (uint32_t)(s_hi - h_lo);
-  const uint32_t rend = (uint32_t)(P.end - h_lo);  // bytes available (for hashing)
+  const uint32_t rend = (uint32_t)(f_end - h_lo);  // bytes available (for hashing)
   Key key;
   key.kmask = P.klen >= 4 ? 0xFFFFFFFFu : 0xFFFFFFu;
   key.kmask2 = P.klen >= 8 ? 0xFFFFFFFFu : P.klen == 6 ? 0xFFFFu : P.klen == 5 ? 0xFFu : 0u;
@@ -1120,7 +1134,7 @@ __global__ __launch_bounds__(64) void price_kernel(DeflateParams P) {
   const int lane = threadIdx.x;
   const uint32_t blk = blockIdx.x;
   const uint64_t lo = (uint64_t)blk * DF_BLOCK;
-  const uint64_t n = P.end - P.halo;
+  const uint64_t n = stream_end(P, blk);
   const uint32_t blen = (uint32_t)((n - lo) < DF_BLOCK ? (n - lo) : DF_BLOCK);
   for (int i = lane; i < 288; i += 64) s->lit_hist[i] = 0;
   if (lane < 32) s->dist_hist[lane] = 0;
@@ -1171,7 +1185,7 @@ __global__ __launch_bounds__(64) void optparse_kernel(DeflateParams P) {
   const int lane = threadIdx.x;
   const uint32_t blk = blockIdx.x;
   const uint64_t lo = (uint64_t)blk * DF_BLOCK;
-  const uint64_t n = P.end - P.halo;
+  const uint64_t n = stream_end(P, blk);
   const uint32_t blen = (uint32_t)((n - lo) < DF_BLOCK ? (n - lo) : DF_BLOCK);
   const uint8_t *data = P.base + P.halo + lo;
   uint32_t *r_blk = P.res + lo;
@@ -1301,12 +1315,12 @@ __global__ __launch_bounds__(64) void block_kernel(DeflateParams P) {
   const int lane = threadIdx.x;
   const uint32_t blk = blockIdx.x;
   const uint64_t lo = (uint64_t)blk * DF_BLOCK;
-  const uint64_t n = P.end - P.halo;
+  const uint64_t n = stream_end(P, blk);
   const uint32_t blen = (uint32_t)((n - lo) < DF_BLOCK ? (n - lo) : DF_BLOCK);
   const uint8_t *data = P.base + P.halo + lo;
   uint32_t *r_blk = P.res + lo;
   BlockPlan *plan = P.plans + blk;
-  const bool last = P.final_ && (blk == P.nblocks - 1);
+  const bool last = P.span ? lo + DF_BLOCK >= n : P.final_ && (blk == P.nblocks - 1);
   for (int i = lane; i < 288; i += 64) s->lit_hist[i] = 0;
   if (lane < 32) s->dist_hist[lane] = 0;
   wsync();
@@ -1764,19 +1778,24 @@ __global__ __launch_bounds__(ENC_THREADS) void encode_kernel(DeflateParams P) {
 // (a non-final call -- a shard -- also ends with the marker: the next shard
 // is independent when deflated with halo 0, see zt_shard.py)
 constexpr uint32_t kRestartMarkerLen = 10;
-__device__ __forceinline__ bool restart_after(uint32_t b, uint32_t n, uint32_t restart, int final_) {
+__device__ __forceinline__ bool restart_after(uint32_t b, uint32_t n, uint32_t restart, int final_,
+                                              const uint64_t *span) {
+  if (span) {  // batch: inside a stream only (its last block carries BFINAL)
+    const uint64_t nx = (uint64_t)(b + 1) * DF_BLOCK;
+    return nx < span[2 * (uint64_t)b + 1] && ((nx - span[2 * (uint64_t)b]) / DF_BLOCK) % restart == 0;
+  }
   return (b + 1 < n) ? ((b + 1) % restart) == 0 : !final_;
 }
 
 __global__ __launch_bounds__(1024) void scan_sizes(const uint32_t *__restrict__ len, uint32_t n,
                                                    uint64_t *__restrict__ off, uint64_t base, uint32_t restart,
-                                                   int final_) {
+                                                   int final_, const uint64_t *__restrict__ span) {
   __shared__ uint64_t part[1024];
   const uint32_t t = threadIdx.x;
   const uint32_t per = (n + 1023) / 1024;
   const uint32_t a = t * per, b = (a + per) < n ? (a + per) : n;
   uint64_t sum = 0;
-  for (uint32_t i = a; i < b; ++i) sum += len[i] + (restart_after(i, n, restart, final_) ? kRestartMarkerLen : 0);
+  for (uint32_t i = a; i < b; ++i) sum += len[i] + (restart_after(i, n, restart, final_, span) ? kRestartMarkerLen : 0);
   part[t] = sum;
   __syncthreads();
   for (int d = 1; d < 1024; d <<= 1) {
@@ -1788,19 +1807,20 @@ __global__ __launch_bounds__(1024) void scan_sizes(const uint32_t *__restrict__ 
   uint64_t run = base + part[t] - sum;
   for (uint32_t i = a; i < b; ++i) {
     off[i] = run;
-    run += len[i] + (restart_after(i, n, restart, final_) ? kRestartMarkerLen : 0);
+    run += len[i] + (restart_after(i, n, restart, final_, span) ? kRestartMarkerLen : 0);
   }
   if (t == 1023) off[n] = base + part[1023];
 }
 
 __global__ __launch_bounds__(256) void gather_blocks(const uint8_t *__restrict__ slots, const uint32_t *__restrict__ len,
                                                      const uint64_t *__restrict__ off, uint8_t *__restrict__ out,
-                                                     uint32_t nblocks, uint32_t restart, int final_) {
+                                                     uint32_t nblocks, uint32_t restart, int final_,
+                                                     const uint64_t *__restrict__ span) {
   const uint32_t b = blockIdx.x;
   const uint8_t *src = slots + (size_t)b * DF_SLOT;
   uint8_t *dst = out + off[b];
   const uint32_t n = len[b];
-  if (restart_after(b, nblocks, restart, final_) && threadIdx.x < kRestartMarkerLen) {
+  if (restart_after(b, nblocks, restart, final_, span) && threadIdx.x < kRestartMarkerLen) {
     const uint32_t i = threadIdx.x % 5;
     dst[n + threadIdx.x] = i < 3 ? 0 : 0xFF;
   }
@@ -1964,6 +1984,7 @@ int deflate_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t halo, in
   P.good = L.good;
   P.ctype = ctype;
   P.opt = L.opt && ctype == 2;
+  P.span = nullptr;
   P.res = reinterpret_cast<uint32_t *>(sb);
   P.slots = sb + G.res_bytes;
   P.slot_len = reinterpret_cast<uint32_t *>(sb + G.res_bytes + G.slot_bytes);
@@ -1984,9 +2005,9 @@ int deflate_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t halo, in
   ZT_HIP(hipGetLastError());
   encode_kernel<<<G.nblocks, ENC_THREADS, 0, s>>>(P);
   ZT_HIP(hipGetLastError());
-  scan_sizes<<<1, 1024, 0, s>>>(P.slot_len, G.nblocks, off, 0, P.restart, final_);
+  scan_sizes<<<1, 1024, 0, s>>>(P.slot_len, G.nblocks, off, 0, P.restart, final_, nullptr);
   ZT_HIP(hipGetLastError());
-  gather_blocks<<<G.nblocks, 256, 0, s>>>(P.slots, P.slot_len, off, d_out, G.nblocks, P.restart, final_);
+  gather_blocks<<<G.nblocks, 256, 0, s>>>(P.slots, P.slot_len, off, d_out, G.nblocks, P.restart, final_, nullptr);
   ZT_HIP(hipGetLastError());
   ZT_TRY(timing_end(c, s, 1));
   uint64_t total = 0;
@@ -1995,6 +2016,99 @@ int deflate_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t halo, in
   ZT_TRY(timing_collect(c, &c->times.deflate_ms, &c->times.deflate_launches, 0));
   ZT_TRY(timing_collect(c, &c->times.deflate_pipeline_ms, &c->times.deflate_pipelines, 1));
   *out_len = total;
+  return ZT_OK;
+}
+
+// Batch of independent streams in one pipeline (configs C4 / C2's producer):
+// stream f's bytes are at d_in + off[f] (off 32 KiB aligned, increasing, each
+// stream's blocks directly after the previous stream's), len[f] > 0.  Every
+// workgroup of the match kernel takes one block, so a stream's history never
+// reaches into another; each stream's last block carries BFINAL and restart
+// markers stay inside streams.  Stream f's bytes land at d_out +
+// out_off[f] .. out_off[f + 1] (host array of count + 1).
+size_t deflate_batch_scratch_bytes(const DeviceCtx *c, size_t padded) {
+  DeflateGeom G;
+  const size_t base = deflate_geometry(c, padded, &G);
+  return base + (((size_t)G.nblocks * 16 + 255) & ~size_t(255));
+}
+
+int deflate_batch_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t count, const uint64_t *off, const uint64_t *len,
+                          int ctype, int level, uint8_t *d_out, uint64_t *out_off, void *scratch_base,
+                          size_t scratch_size, hipStream_t s) {
+  if (count == 0) return ZT_OK;
+  const uint64_t padded = off[count - 1] + ((len[count - 1] + DF_BLOCK - 1) / DF_BLOCK) * DF_BLOCK;
+  DeflateGeom G;
+  const size_t need = deflate_geometry(c, padded, &G);
+  const size_t span_bytes = ((size_t)G.nblocks * 16 + 255) & ~size_t(255);
+  if (need + span_bytes > scratch_size) return set_error(ZT_E_NOMEM, "deflate scratch too small");
+  uint8_t *sb = static_cast<uint8_t *>(scratch_base);
+  std::vector<uint64_t> span((size_t)G.nblocks * 2, 0);
+  std::vector<uint32_t> first(count);
+  for (size_t f = 0; f < count; ++f) {
+    const uint64_t b0 = off[f] / DF_BLOCK, nb = (len[f] + DF_BLOCK - 1) / DF_BLOCK;
+    if (off[f] % DF_BLOCK || len[f] == 0 || (f && b0 * DF_BLOCK != off[f - 1] + ((len[f - 1] + DF_BLOCK - 1) / DF_BLOCK) * DF_BLOCK))
+      return set_error(ZT_E_ARG, "batch streams must be non-empty and packed at 32 KiB boundaries");
+    first[f] = (uint32_t)b0;
+    for (uint64_t b = b0; b < b0 + nb; ++b) {
+      span[2 * b] = off[f];
+      span[2 * b + 1] = off[f] + len[f];
+    }
+  }
+  uint64_t *d_span = reinterpret_cast<uint64_t *>(sb + need);
+  ZT_HIP(hipMemcpyAsync(d_span, span.data(), span.size() * 8, hipMemcpyHostToDevice, s));
+  DeflateParams P;
+  P.base = d_in;
+  P.halo = 0;
+  P.end = padded;
+  P.blocks_per_wg = 1;
+  P.nblocks = G.nblocks;
+  P.restart = restart_blocks();
+  P.hist_max = DF_HIST;
+  P.final_ = 1;
+  const DeflateLevel L = level_params(level);
+  P.max_chain = L.max_chain;
+  P.nice_len = L.nice;
+  P.lazy = L.lazy;
+  P.too_far = L.too_far;
+  P.skip_len = L.skip;
+  P.klen = L.klen;
+  P.probe = L.probe;
+  P.good = L.good;
+  P.ctype = ctype;
+  P.opt = L.opt && ctype == 2;
+  P.span = d_span;
+  P.res = reinterpret_cast<uint32_t *>(sb);
+  P.slots = sb + G.res_bytes;
+  P.slot_len = reinterpret_cast<uint32_t *>(sb + G.res_bytes + G.slot_bytes);
+  uint64_t *d_off = reinterpret_cast<uint64_t *>(sb + G.res_bytes + G.slot_bytes + G.len_bytes);
+  P.plans = reinterpret_cast<BlockPlan *>(sb + G.res_bytes + G.slot_bytes + G.len_bytes + G.off_bytes);
+  ZT_TRY(timing_begin(c, s, 1));
+  ZT_TRY(timing_begin(c, s, 0));
+  match_kernel<<<G.nblocks, DF_THREADS, 0, s>>>(P);
+  ZT_HIP(hipGetLastError());
+  ZT_TRY(timing_end(c, s, 0));
+  if (P.opt) {
+    price_kernel<<<G.nblocks, 64, 0, s>>>(P);
+    ZT_HIP(hipGetLastError());
+    optparse_kernel<<<G.nblocks, 64, 0, s>>>(P);
+    ZT_HIP(hipGetLastError());
+  }
+  block_kernel<<<G.nblocks, 64, 0, s>>>(P);
+  ZT_HIP(hipGetLastError());
+  encode_kernel<<<G.nblocks, ENC_THREADS, 0, s>>>(P);
+  ZT_HIP(hipGetLastError());
+  scan_sizes<<<1, 1024, 0, s>>>(P.slot_len, G.nblocks, d_off, 0, P.restart, 1, d_span);
+  ZT_HIP(hipGetLastError());
+  gather_blocks<<<G.nblocks, 256, 0, s>>>(P.slots, P.slot_len, d_off, d_out, G.nblocks, P.restart, 1, d_span);
+  ZT_HIP(hipGetLastError());
+  ZT_TRY(timing_end(c, s, 1));
+  std::vector<uint64_t> boff((size_t)G.nblocks + 1);
+  ZT_HIP(hipMemcpyAsync(boff.data(), d_off, boff.size() * 8, hipMemcpyDeviceToHost, s));
+  ZT_HIP(hipStreamSynchronize(s));
+  ZT_TRY(timing_collect(c, &c->times.deflate_ms, &c->times.deflate_launches, 0));
+  ZT_TRY(timing_collect(c, &c->times.deflate_pipeline_ms, &c->times.deflate_pipelines, 1));
+  for (size_t f = 0; f < count; ++f) out_off[f] = boff[first[f]];
+  out_off[count] = boff[G.nblocks];
   return ZT_OK;
 }
 

@@ -120,17 +120,6 @@ int zt_deflate_raw(const uint8_t *in, size_t n, const zt_deflate_opts *opts, uin
   return ZT_OK;
 }
 
-int zt_deflate_raw_batch(const uint8_t *const *in, const size_t *n, size_t count, const zt_deflate_opts *opts,
-                         uint8_t **out, size_t *out_len, int *status) {
-  if (!in || !n || !out || !out_len || !status) return set_error(ZT_E_ARG, "null argument");
-  int first = ZT_OK;
-  for (size_t i = 0; i < count; ++i) {
-    status[i] = zt_deflate_raw(in[i], n[i], opts, &out[i], &out_len[i]);
-    if (status[i] && first == ZT_OK) first = status[i];
-  }
-  return first;
-}
-
 int zt_inflate_plan_create(size_t max_in, size_t max_out, zt_inflate_plan **plan) {
   if (!plan) return set_error(ZT_E_ARG, "null plan");
   DeviceCtx *c;
@@ -164,7 +153,8 @@ int zt_inflate_dev(zt_inflate_plan *plan, const void *d_in, size_t n, void *d_ou
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   uint8_t *o = (uint8_t *)d_out;
   size_t ol = 0, eip = 0;
-  const int seg = inflate_segments_dev(c, (const uint8_t *)d_in, n, 0, &o, out_cap, &ol, &eip, s);
+  int seg = inflate_segments_dev(c, (const uint8_t *)d_in, n, 0, &o, out_cap, &ol, &eip, s);
+  if (seg == 1) seg = inflate_general_dev(c, (const uint8_t *)d_in, n, 0, &o, out_cap, &ol, &eip, s);
   if (seg < 0) return seg;
   if (seg == 0) {
     *out_len = ol;

@@ -135,6 +135,7 @@ static int batch_two_phase(DeviceCtx *c, const uint8_t *d_in, const std::vector<
   rp.seg_status = d_st;
   rp.nunits = (uint32_t)chain.size();
   rp.nseg = (uint32_t)segs.size();
+  rp.marker = 0;
   ZT_TRY(resolve_segments_dev(rp, s));
   std::vector<int32_t> ust(chain.size()), sst(segs.size());
   ZT_HIP(hipMemcpyAsync(ust.data(), d_ust, chain.size() * 4, hipMemcpyDeviceToHost, s));
@@ -232,6 +233,7 @@ static int inflate_host_batch(const uint8_t *const *in, const size_t *n, const s
     }
     ZT_HIP(hipMemcpyAsync(d_jobs, jobs.data(), todo.size() * sizeof(InfJob), hipMemcpyHostToDevice, c->stream));
     ZT_TRY(inflate_jobs_dev((const InfJob *)d_jobs, (InfResult *)d_res, (int)todo.size(), c->stream));
+    if (pass == 0) c->times.inflate_paths[2] += todo.size();
     std::vector<InfResult> r(todo.size());
     ZT_HIP(hipMemcpyAsync(r.data(), d_res, todo.size() * sizeof(InfResult), hipMemcpyDeviceToHost, c->stream));
     ZT_HIP(hipStreamSynchronize(c->stream));
@@ -298,7 +300,9 @@ int zt_inflate_raw(const uint8_t *in, size_t n, size_t index, const zt_inflate_o
     ZT_HIP(hipMemcpyAsync(d_in, in, n, hipMemcpyHostToDevice, c->stream));
     uint8_t *d_out = nullptr;
     size_t ol = 0, eip = 0;
-    const int seg = inflate_segments_dev(c, (const uint8_t *)d_in, n, index, &d_out, 0, &ol, &eip, c->stream);
+    int seg = inflate_segments_dev(c, (const uint8_t *)d_in, n, index, &d_out, 0, &ol, &eip, c->stream);
+    // no sync points: speculative parallel decode at arbitrary bit offsets
+    if (seg == 1) seg = inflate_general_dev(c, (const uint8_t *)d_in, n, index, &d_out, 0, &ol, &eip, c->stream);
     if (seg < 0) return seg;
     if (seg == 0) {
       uint8_t *h = (uint8_t *)malloc(ol ? ol : 1);

@@ -340,6 +340,7 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   rp.seg_status = d_st;
   rp.nunits = (uint32_t)chain.size();
   rp.nseg = (uint32_t)segs.size();
+  rp.marker = 0;
   ZT_TRY(resolve_segments_dev(rp, s));
   ZT_TRY(timing_end(c, s, 2));
   ZT_HIP(hipMemcpyAsync(h_ust, d_ust, chain.size() * 4, hipMemcpyDeviceToHost, s));
@@ -351,6 +352,7 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
     if (h_ust[i] != ZT_OK) FALLBACK("unit %zu of %zu (chain): status %d\n", i, chain.size(), h_ust[i]);
   for (size_t i = 0; i < segs.size(); ++i)
     if (h_st[i] != ZT_OK) FALLBACK("segment %zu of %zu: status %d\n", i, segs.size(), h_st[i]);
+  c->times.inflate_paths[0]++;
   return ZT_OK;
 }
 

@@ -1,0 +1,504 @@
+// inflate_simt.h -- Huffman block bodies to tokens, shared by the sync-point
+// tokenizer (inflate_tok.hip) and the general speculative tokenizer
+// (inflate_gen.hip): the lane-uniform scalar decoder and the 64-lane
+// speculative (SIMT) decoder.  Follows src/RawInflate.ts:466-516.
+#pragma once
+#include "inflate_common.h"
+
+namespace zt {
+namespace {
+
+// token staging: lane k of `stg` holds token (ntok & ~63) + k of the current
+// group of 64; a full group is written with one coalesced 256-byte store
+struct TokOut {
+  uint32_t *tok;
+  uint32_t cap;
+  uint32_t ntok;
+  uint32_t stg;
+  int lane;
+
+  __device__ __forceinline__ void emit(uint32_t t) {
+    const uint32_t k = uni(ntok);
+    if (lane == (int)(k & 63)) stg = t;
+    ntok = k + 1;
+    if (((k + 1) & 63) == 0) tok[k - 63 + lane] = stg;
+  }
+  __device__ __forceinline__ void flush_partial() {
+    const uint32_t c = ntok & 63;
+    if (lane < (int)c) tok[(ntok & ~63u) + lane] = stg;
+  }
+};
+
+// code longer than PRI bits: canonical search (src/Huffman.ts semantics)
+__device__ __forceinline__ int long_code(const HuffTab *t, uint32_t v, uint32_t &len) {
+  const uint32_t r = __brev(v);
+  const int ml = (int)uni((uint32_t)t->maxlen);
+  for (int l = PRI + 1; l <= ml; ++l) {
+    const uint32_t c = r >> (32 - l);
+    const uint32_t k = c - uni(t->first[l]);
+    if (k < uni(t->count[l])) {
+      len = (uint32_t)l;
+      return (int)uni(t->sorted[uni(t->offs[l]) + k]);
+    }
+  }
+  return -1;
+}
+
+// Huffman block body -> tokens (non-strict reader).  Returns 0 at end of
+// block, or a status.
+__device__ __forceinline__ int tok_huffman(Reader &rd, const HuffTab *lt, const HuffTab *dt, TokOut &to,
+                                           uint64_t &op) {
+  const uint64_t hib = uni64(rd.hi) * 8;
+  constexpr uint32_t M = (1u << PRI) - 1;
+  for (;;) {
+    rd.refill();  // >= 56 valid bits: one token needs at most 15 + 5 + 15 + 13
+    const uint64_t bb = uni64(rd.bb);
+    const uint32_t e = uni(lt->pri[(uint32_t)bb & M]);
+    uint32_t cl, sym, ex, base;
+    if (e & 15) {
+      cl = e & 15;
+      sym = (e >> 8) & 511;
+      ex = (e >> 4) & 15;
+      base = e >> 17;
+    } else {
+      const int s = long_code(lt, (uint32_t)bb, cl);
+      if (s < 0) return ZT_E_INVALID_SYMBOL;
+      sym = (uint32_t)s;
+      ex = sym > 256 ? len_extra(sym - 257) : 0;
+      base = sym > 256 ? len_base(sym - 257) : 0;
+    }
+    if (sym < 256) {
+      if (to.ntok >= to.cap) return ZT_E_NOMEM;
+      rd.bb = bb >> cl;
+      rd.bc -= cl;
+      to.emit(sym);
+      op += 1;
+      if (rd.pos_bits() > hib) return ZT_E_INPUT_BROKEN;
+      continue;
+    }
+    if (sym == 256) {
+      rd.bb = bb >> cl;
+      rd.bc -= cl;
+      if (rd.pos_bits() > hib) return ZT_E_INPUT_BROKEN;
+      return ZT_OK;
+    }
+    const uint32_t length = base + ((uint32_t)(bb >> cl) & ((1u << ex) - 1));
+    uint32_t used = cl + ex;
+    const uint64_t b2 = bb >> used;
+    const uint32_t d = uni(dt->pri[(uint32_t)b2 & M]);
+    uint32_t dcl, dsym, dex, dbase;
+    if (d & 15) {
+      dcl = d & 15;
+      dsym = (d >> 8) & 511;
+      dex = (d >> 4) & 15;
+      dbase = d >> 17;
+    } else {
+      const int s = long_code(dt, (uint32_t)b2, dcl);
+      if (s < 0) return ZT_E_INVALID_SYMBOL;
+      dsym = (uint32_t)s;
+      dex = dsym < 30 ? dist_extra(dsym) : 0;
+      dbase = dsym < 30 ? dist_base(dsym) : 0;
+    }
+    if (dsym >= 30) return ZT_E_INVALID_SYMBOL;
+    const uint32_t dist = dbase + ((uint32_t)(b2 >> dcl) & ((1u << dex) - 1));
+    used += dcl + dex;
+    rd.bb = bb >> used;
+    rd.bc -= used;
+    if (rd.pos_bits() > hib) return ZT_E_INPUT_BROKEN;
+    if (to.ntok >= to.cap) return ZT_E_NOMEM;
+    to.emit((length << 16) | dist);
+    op += length;
+  }
+}
+
+
+// ------------------------------------------------ phase A, SIMT block body
+// A Huffman block body is decoded by all 64 lanes at once, in rounds of
+// 64 x SP_LANE_BITS bits, each lane from its own bit offset (speculative
+// parallel decoding of a prefix code).  Lane l starts at s_l and decodes until
+// it passes s_{l+1}, marking in a bitmap every position where a token began.
+// Decoding is deterministic, so once a lane's path meets the true token
+// sequence it *is* the true sequence.  The true start of lane l is the end of
+// lane l-1's true path; if that position is marked in lane l's bitmap, lane l
+// is synchronised and its tokens are the marks from there on (popcount).
+// DEFLATE token streams often take tens of tokens to resynchronise (extra
+// bits are raw), so unsynchronised lanes are re-decoded in parallel from
+// their true start until they merge with their old path (a marked position),
+// and the marks are corrected on the way.  A second pass decodes every lane's
+// exact range and writes its tokens at their final index.
+#ifndef ZT_SP_LANE_BITS
+#define ZT_SP_LANE_BITS 480
+#endif
+constexpr uint32_t SP_LANE_BITS = ZT_SP_LANE_BITS;        // 60 bytes per lane: 18.5 KiB of LDS, 8 units per CU
+constexpr uint32_t SP_WORDS = SP_LANE_BITS / 32;          // bitmap words per lane
+constexpr uint32_t SP_STAGE_BYTES = IN_RING;              // staged input per round
+static_assert(64 * SP_LANE_BITS / 8 + 16 + 64 <= SP_STAGE_BYTES, "round must fit the stage");
+static_assert(SP_STAGE_BYTES <= 4 * IN_RING_WORDS, "stage lives in the reader's ring");
+
+struct SpecShared {
+  uint32_t bm[SP_WORDS][64];  // token-start bitmap, word w of lane l
+  uint32_t tail[64];          // the unit's last partial token group (staging)
+};
+
+// per-lane bit reader over the round's staged input (LDS, dword q at
+// stage[q - qbase])
+struct LaneBits {
+  const uint32_t *stage;
+  uint32_t qbase;
+  uint32_t q;      // next dword to shift in
+  uint64_t bb;
+  uint32_t bc;
+  uint32_t rel;    // bit position of bb bit 0, relative to the body start
+
+  __device__ __forceinline__ uint32_t word(uint32_t qq) const {
+    return stage[(qq - qbase) & (SP_STAGE_BYTES / 4 - 1)];
+  }
+  // abs_bit: relative to the reader's abase; rel0: the same, relative to the body
+  __device__ __forceinline__ void init(uint64_t abs_bit, uint32_t rel0) {
+    q = (uint32_t)(abs_bit >> 5);
+    const uint32_t sh = (uint32_t)abs_bit & 31;
+    bb = word(q) >> sh;
+    bc = 32 - sh;
+    ++q;
+    rel = rel0;
+  }
+  // afterwards at least 32 valid bits
+  __device__ __forceinline__ void refill() {
+    if (bc <= 32) {
+      bb |= (uint64_t)word(q) << bc;
+      bc += 32;
+      ++q;
+    }
+  }
+  __device__ __forceinline__ void consume(uint32_t n) {
+    bb >>= n;
+    bc -= n;
+    rel += n;
+  }
+};
+
+// code longer than PRI bits, per lane
+// (canonical limits: the length is one more than the number of lengths
+// whose left-justified code range ends at or below the peek; all limits are
+// read at once instead of a length-by-length search)
+__device__ __forceinline__ int long_code_lane(const HuffTab *t, uint32_t v, uint32_t &len) {
+  const uint64_t r = __brev(v);
+  uint32_t l = PRI + 1;
+#pragma unroll
+  for (int k = PRI + 1; k < 16; ++k) l += r >= t->lim[k] ? 1u : 0u;
+  if (l > (uint32_t)t->maxlen) return -1;
+  len = l;
+  return (int)t->sorted[t->base[l] + (int32_t)((uint32_t)r >> (32 - l))];
+}
+
+// one token at the lane's position: 0 ok (tok, nbytes), 1 end of block, -1 invalid
+__device__ __forceinline__ int lane_token(LaneBits &lb, const HuffTab *lt, const HuffTab *dt, uint32_t &tok,
+                                          uint32_t &nbytes) {
+  constexpr uint32_t M = (1u << PRI) - 1;
+  lb.refill();
+  const uint32_t e = lt->pri[(uint32_t)lb.bb & M];
+  uint32_t cl, sym, ex, base;
+  if (e & 15) {
+    cl = e & 15;
+    sym = (e >> 8) & 511;
+    ex = (e >> 4) & 15;
+    base = e >> 17;
+  } else {
+    const int s = long_code_lane(lt, (uint32_t)lb.bb, cl);
+    if (s < 0) return -1;
+    sym = (uint32_t)s;
+    ex = sym > 256 ? len_extra(sym - 257) : 0;
+    base = sym > 256 ? len_base(sym - 257) : 0;
+  }
+  if (sym < 256) {
+    lb.consume(cl);
+    tok = sym;
+    nbytes = 1;
+    return 0;
+  }
+  if (sym == 256) {
+    lb.consume(cl);
+    return 1;
+  }
+  const uint32_t length = base + ((uint32_t)(lb.bb >> cl) & ((1u << ex) - 1));
+  lb.consume(cl + ex);
+  lb.refill();
+  const uint32_t d = dt->pri[(uint32_t)lb.bb & M];
+  uint32_t dcl, dsym, dex, dbase;
+  if (d & 15) {
+    dcl = d & 15;
+    dsym = (d >> 8) & 511;
+    dex = (d >> 4) & 15;
+    dbase = d >> 17;
+  } else {
+    const int s = long_code_lane(dt, (uint32_t)lb.bb, dcl);
+    if (s < 0) return -1;
+    dsym = (uint32_t)s;
+    dex = dsym < 30 ? dist_extra(dsym) : 0;
+    dbase = dsym < 30 ? dist_base(dsym) : 0;
+  }
+  if (dsym >= 30) return -1;
+  const uint32_t dist = dbase + ((uint32_t)(lb.bb >> dcl) & ((1u << dex) - 1));
+  lb.consume(dcl + dex);
+  tok = (length << 16) | dist;
+  nbytes = length;
+  return 0;
+}
+
+// lane l-1's value (lane 0: `first`), with every lane taking part (DPP wave_shr:1)
+__device__ __forceinline__ uint32_t from_prev_lane(uint32_t v, uint32_t first) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)first, (int)v, 0x138, 0xF, 0xF, false);
+}
+
+// Decode the body of a Huffman block that starts at bit `b0` (relative to
+// rd's abase) with the tables in lt / dt.  Tokens go to to.tok[to.ntok ...].
+// Returns 0 with *end_bit = the bit after the end-of-block code, 1 when the
+// body is too large for this path, or a status.
+// stop_rel (bits from b0): decoding also ends at the first token that starts
+// at or after it (*stopped = true, *end_bit = that token's start, the token
+// not decoded).  bm_out (global, SP_WORDS * 64 words): the token-start bitmap
+// of the path's first round (bit x = a token starts at b0 + x), for the
+// speculative tokenizer's sync test.
+__device__ int tok_huffman_simt(Reader &rd, uint64_t b0, const HuffTab *lt, const HuffTab *dt, TokOut &to,
+                                uint64_t &op, SpecShared *sp, uint64_t &end_bit, uint32_t *dump = nullptr,
+                                uint32_t stop_rel = 0xFFFFFFFFu, uint32_t *bm_out = nullptr,
+                                bool *stopped = nullptr) {
+  const int lane = to.lane;
+  // bits available after b0 (positions are u32: a body past 2^31 bits -- a
+  // 256 MiB single block -- runs into the limit and is reported as broken,
+  // which sends the stream to the one-wave decoder)
+  const uint64_t lim = uni64(rd.hi) * 8 - b0;
+  const uint32_t limit = lim < 0x7FFFFFFFull ? (uint32_t)lim : 0x7FFFFFFFu;
+  uint32_t *stage = rd.inbuf;  // the reader's ring is reloaded afterwards
+  LaneBits lb;
+  lb.stage = stage;
+  uint32_t R = 0;  // true start of this round (bits from b0)
+  int dump_round = 0;
+  for (;;) {
+    // ---- stage the round's input: bytes [a0, a0 + SP_STAGE_BYTES)
+    const uint64_t a0 = ((b0 + R) >> 3) & ~uint64_t(15);
+    {
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      typedef __attribute__((address_space(1))) const u32x4 g_u32x4;
+      const uint64_t hi = uni64(rd.hi);
+#pragma unroll
+      for (uint32_t k = 0; k < SP_STAGE_BYTES / 1024; ++k) {
+        const uint64_t off = a0 + k * 1024 + (uint32_t)lane * 16;
+        u32x4 v = {0, 0, 0, 0};
+        if (off < hi) v = *(g_u32x4 *)(rd.abase + off);
+        const uint32_t w = k * 256 + (uint32_t)lane * 4;
+        stage[w] = v.x;
+        stage[w + 1] = v.y;
+        stage[w + 2] = v.z;
+        stage[w + 3] = v.w;
+      }
+      lb.qbase = (uint32_t)(a0 >> 2);
+    }
+    for (uint32_t w = 0; w < SP_WORDS; ++w) sp->bm[w][lane] = 0;
+    wave_sync();
+    // ---- pass 1: lane l from s_l past s_{l+1}, marking token starts
+    const uint32_t s_l = R + (uint32_t)lane * SP_LANE_BITS;
+    const uint32_t s_next = s_l + SP_LANE_BITS;
+    const bool in_range = s_l < limit;
+    uint32_t end = s_l, ev_pos = 0;  // ev_pos: start of the EOB / invalid token
+    int flags = 0;                   // 1 end of block, 2 invalid, 3 stop position reached
+    bool todo = in_range;
+    uint32_t from = s_l;             // where this lane's current decode starts
+    bool repair = false;
+    for (int iter = 0;; ++iter) {
+      if (iter > 66) return ZT_E_INPUT_BROKEN;
+      bool active = todo;
+      uint32_t cw = 0, cwi = 0;  // bitmap word being assembled, its index
+      uint32_t merge = 0xFFFFFFFFu;
+      if (active) {
+        lb.init(b0 + from, from);
+        cwi = (from - s_l) >> 5;
+        cw = 0;
+        if (!repair) flags = 0;
+        // marks below a repair's start are off every path it can merge with
+        for (uint32_t x = 0; x < cwi; ++x) sp->bm[x][lane] = 0;
+      }
+      while (__ballot(active)) {
+        if (active) {
+          const uint32_t p = lb.rel - s_l;  // < SP_LANE_BITS while decoding this lane's range
+          const uint32_t wi = p >> 5;
+          if (wi != cwi) {
+            // leave word cwi: new marks below, on a repair old marks are stale
+            sp->bm[cwi][lane] = cw;
+            for (uint32_t x = cwi + 1; x < wi; ++x) sp->bm[x][lane] = 0;
+            cwi = wi;
+            cw = 0;
+          }
+          if (repair && ((sp->bm[wi][lane] >> (p & 31)) & 1)) {
+            // merged with the old path: the old marks from p on are right
+            merge = p;
+            const uint32_t below = (p & 31) ? (0xFFFFFFFFu >> (32 - (p & 31))) : 0u;
+            sp->bm[wi][lane] = (cw & below) | (sp->bm[wi][lane] & ~below);
+            active = false;
+          } else {
+            cw |= 1u << (p & 31);
+            uint32_t tk, nb;
+            if (lb.rel >= stop_rel) {
+              // a token starts at or after the stop: the unit ends here
+              flags = 3;
+              ev_pos = s_l + p;
+              end = ev_pos;
+              active = false;
+            } else {
+            const int r = lane_token(lb, lt, dt, tk, nb);
+            if (r != 0 || lb.rel > limit) {
+              flags = r > 0 ? 1 : 2;
+              ev_pos = lb.rel - 0;  // provisional; fixed below
+              ev_pos = s_l + p;
+              end = lb.rel;
+              active = false;
+            } else if (lb.rel >= s_next) {
+              end = lb.rel;
+              flags = 0;
+              active = false;
+            }
+            }
+            if (!active) {
+              sp->bm[cwi][lane] = cw;
+              for (uint32_t x = cwi + 1; x < SP_WORDS; ++x) sp->bm[x][lane] = 0;
+            }
+          }
+        }
+      }
+      wave_sync();
+      // ---- which lanes are on the true path?
+      const uint32_t t = from_prev_lane(end, R);
+      const uint32_t tp = t - s_l;
+      const bool synced = in_range && t >= s_l && tp < SP_LANE_BITS && ((sp->bm[tp >> 5][lane] >> (tp & 31)) & 1);
+      const uint64_t U = __ballot(!synced);
+      const uint64_t E = __ballot(synced && flags != 0 && ev_pos >= t);
+      const int f = U ? __builtin_ctzll(U) : 64;
+      const int e = E ? __builtin_ctzll(E) : 64;
+      if (e < f) {
+        // the block ends (or breaks) in lane e
+        if (__builtin_amdgcn_readlane(flags, e) == 2) return ZT_E_INVALID_SYMBOL;
+        break;
+      }
+      if (f == 64) break;  // every lane synchronised, the block continues
+      if (!__builtin_amdgcn_readlane((int)in_range, f)) return ZT_E_INPUT_BROKEN;  // runs past the input
+      // re-decode every unsynchronised lane from its (current) true start
+      // (a lane whose predecessor stopped short of it waits: that predecessor
+      // is off the true path and is repaired first)
+      todo = in_range && !synced && t >= s_l && tp < SP_LANE_BITS;
+      if (todo) from = t;
+      repair = true;
+      (void)merge;
+    }
+    // final per-lane state: true start t, tokens = marks in [t, ev or end)
+    const uint32_t t = from_prev_lane(end, R);
+    const uint64_t E = __ballot(flags != 0 && ev_pos >= t && in_range);
+    const int e = E ? __builtin_ctzll(E) : 64;
+    const int last = e < 64 ? e : 63;
+    const bool eob = e < 64;
+    const bool use = lane <= last;
+    uint32_t my_tok = 0;
+    if (use) {
+      const uint32_t lo = t - s_l;
+      const uint32_t hi_p = (lane == e) ? ev_pos - s_l : SP_LANE_BITS;  // marks at p < hi_p
+      for (uint32_t w = lo >> 5; w < SP_WORDS && w * 32 < hi_p; ++w) {
+        uint32_t m = sp->bm[w][lane];
+        if (w == (lo >> 5)) m &= 0xFFFFFFFFu << (lo & 31);
+        if (hi_p < (w + 1) * 32) m &= (hi_p & 31) ? (0xFFFFFFFFu >> (32 - (hi_p & 31))) : 0u;
+        my_tok += __popc(m);
+      }
+    }
+    if (bm_out && R == 0) {
+      // the path's token starts of this first round: lane l's marks in [t, hi_p)
+      const uint32_t lo = t - s_l;
+      const uint32_t hi_p = (lane == e) ? ev_pos - s_l : SP_LANE_BITS;
+      for (uint32_t w = 0; w < SP_WORDS; ++w) {
+        uint32_t m = use ? sp->bm[w][lane] : 0u;
+        if (w * 32 + 32 <= lo) m = 0;
+        else if (w * 32 < lo) m &= 0xFFFFFFFFu << (lo & 31);
+        if (hi_p <= w * 32) m = 0;
+        else if (hi_p < (w + 1) * 32) m &= 0xFFFFFFFFu >> (32 - (hi_p & 31));
+        bm_out[lane * SP_WORDS + w] = m;
+      }
+    }
+    if (dump && dump_round < 8) {
+      uint32_t *d = dump + (dump_round * 64 + lane) * 8;
+      d[0] = R;
+      d[1] = t;
+      d[2] = end;
+      d[3] = my_tok;
+      d[4] = (uint32_t)e;
+      d[5] = (uint32_t)flags;
+      d[6] = (uint32_t)last;
+      d[7] = ev_pos;
+      ++dump_round;
+    }
+    uint32_t tok_incl = my_tok;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t a = __shfl_up(tok_incl, off, 64);
+      if (lane >= off) tok_incl += a;
+    }
+    const uint32_t tot_tok = __builtin_amdgcn_readlane(tok_incl, last);
+    const uint32_t nt0 = uni(to.ntok);
+    if ((uint64_t)nt0 + tot_tok > to.cap) return ZT_E_NOMEM;
+    const uint32_t r_end = eob ? __builtin_amdgcn_readlane(end, e) : __builtin_amdgcn_readlane(end, 63);
+    // ---- pass 2: exact ranges, tokens written at their index
+    const uint32_t nt1 = nt0 + tot_tok;
+    const uint32_t tail_base = nt1 & ~63u;
+    to.flush_partial();
+    sp->tail[lane] = to.stg;
+    wave_sync();
+    uint32_t idx = nt0 + tok_incl - my_tok;
+    const uint32_t idx_end = idx + my_tok;
+    uint32_t my_by = 0;
+    bool active = use && my_tok > 0;
+    if (active) lb.init(b0 + t, t);
+    uint32_t *tokp = to.tok;
+    while (__ballot(active)) {
+      if (active) {
+        uint32_t tk = 0, nb = 0;
+        lane_token(lb, lt, dt, tk, nb);
+        tokp[idx] = tk;
+        my_by += nb;
+        if (idx >= tail_base) sp->tail[idx & 63] = tk;
+        if (++idx >= idx_end) active = false;
+      }
+    }
+    wave_sync();
+    uint32_t by = my_by;
+#pragma unroll
+    for (int off = 32; off; off >>= 1) by += __shfl_xor(by, off, 64);
+    to.ntok = nt1;
+    to.stg = sp->tail[lane];
+    op += uni(by);
+    if (eob) {
+      end_bit = b0 + r_end;
+      if (stopped) *stopped = __builtin_amdgcn_readlane(flags, e) == 3;
+      return ZT_OK;
+    }
+    R = r_end;
+  }
+}
+
+// ---- token -> byte resolution constants (inflate_tok.hip, inflate_gen.hip)
+__device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t src_lane) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src_lane << 2), (int)v);
+}
+constexpr uint32_t RS_TOK_RING = 1024;        // tokens staged in LDS (16 chunks of 64)
+constexpr uint32_t RS_AHEAD = 12;             // chunks in flight ahead of the cursor
+constexpr uint32_t RS_FLUSH = 8192;           // output flush granule
+constexpr uint32_t CP_STEP = 256;  // copy_kernel bytes per step
+#ifndef ZT_CP_RING
+#define ZT_CP_RING 2048
+#endif
+#ifndef ZT_CP_AHEAD
+#define ZT_CP_AHEAD 12
+#endif
+constexpr uint32_t CP_DESC_RING = ZT_CP_RING;  // descriptors staged in LDS (chunks of 128)
+constexpr uint32_t CP_AHEAD = ZT_CP_AHEAD;      // chunks in flight ahead of the step
+static_assert((CP_AHEAD + 2) * 128 <= CP_DESC_RING && CP_AHEAD < 64, "descriptor ring");
+// s_waitcnt vmcnt(v) with lgkmcnt / expcnt left alone (vmcnt bits 3:0 and 15:14)
+constexpr int cp_vmcnt(uint32_t v) { return (int)(0x0F70u | (v & 15u) | ((v >> 4) << 14)); }
+
+}  // namespace
+}  // namespace zt

@@ -139,11 +139,35 @@ void parallel_copy(size_t count, const std::function<void(size_t)> &fn, size_t t
   for (auto &x : th) x.join();
 }
 
+int current_device() { return g_dev; }
+
+static std::mutex g_devs_mu;
+static std::vector<int> g_devs;  // zt_set_devices; empty: the calling thread's device
+
+std::vector<int> batch_devices() {
+  std::lock_guard<std::mutex> lk(g_devs_mu);
+  if (g_devs.empty()) return {g_dev};
+  return g_devs;
+}
+
 }  // namespace zt
 
 using namespace zt;
 
 extern "C" {
+
+int zt_set_devices(uint64_t mask) {
+  const int count = zt_device_count();
+  std::vector<int> v;
+  for (int d = 0; d < 64; ++d)
+    if ((mask >> d) & 1) {
+      if (d >= count) return set_error(ZT_E_NO_DEVICE, "invalid device index");
+      v.push_back(d);
+    }
+  std::lock_guard<std::mutex> lk(g_devs_mu);
+  g_devs = v;
+  return ZT_OK;
+}
 
 int zt_device_count(void) {
   int count = 0;

@@ -7,6 +7,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <string>
+#include <vector>
 
 #include "../../include/zt.h"
 
@@ -43,8 +44,8 @@ struct DeviceCtx {
   uint32_t *d_crc_x2n = nullptr;    // x^(2^k) mod P, k = 0..31
   uint32_t *d_crc_shift = nullptr;  // checksum.hip merge constants (crc_shift_tables)
   // scratch
-  void *d_buf[10] = {};  // slot 8: checksum segment partials
-  size_t buf_size[10] = {};
+  void *d_buf[20] = {};  // slot 8: checksum segment partials; 10-17: general inflate (inflate_gen.hip)
+  size_t buf_size[20] = {};
   // second stream: checksums run beside the deflate pipeline in the containers
   hipStream_t aux = nullptr;
   hipEvent_t aux_ev = nullptr;
@@ -137,6 +138,16 @@ void crc_shift_tables(const uint32_t x2n[32], uint32_t shift[ZT_CRC_SHIFT_N]);
 // ---- launchers (device-resident) ------------------------------------------------
 int checksums_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, bool do_crc, bool do_adler, uint32_t crc_in,
                   uint32_t adler_in, uint32_t *d_result /* [2] */, hipStream_t s);
+int checksums_batch_dev(DeviceCtx *c, const uint8_t *frame, size_t count, const uint64_t *off, const uint64_t *len,
+                        uint32_t *d_result /* [2 count] */, hipStream_t s);
+void gzip_header(const zt_gzip_opts *opts, std::vector<uint8_t> &hd);  // container_api.cpp
+int current_device();                                                 // zt_api.cpp (this thread's)
+std::vector<int> batch_devices();                                     // zt_set_devices, else {current}
+// batch deflate (deflate.hip): streams packed at 32 KiB boundaries, one pipeline
+size_t deflate_batch_scratch_bytes(const DeviceCtx *c, size_t padded);
+int deflate_batch_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t count, const uint64_t *off, const uint64_t *len,
+                          int ctype, int level, uint8_t *d_out, uint64_t *out_off, void *scratch_base,
+                          size_t scratch_size, hipStream_t s);
 
 // ---- inflate jobs (one stream per wavefront) -----------------------------------
 struct InfJob {
@@ -220,9 +231,66 @@ struct ResolveParams {
   int32_t *seg_status;   // copy
   uint32_t nunits;
   uint32_t nseg;
+  int32_t marker;        // expand: segments after the first may reach up to 32 KiB behind their start
 };
 int tokenize_units_dev(const TokParams &p, hipStream_t s);
 int resolve_segments_dev(const ResolveParams &p, hipStream_t s);
+int expand_units_dev(const ResolveParams &p, hipStream_t s);
+
+// ---- general speculative inflate (inflate_gen.hip) ---------------------------------
+// A stream without sync points is cut at fixed bit positions; each *unit* is
+// decoded by one wave from a start state that is exact (the stream start, a
+// redo) or guessed (a candidate block header, a stored block's LEN field, or
+// a position inside a block whose header is guessed), up to a stop position.
+enum : uint32_t { GK_BLOCK = 0, GK_HUFF = 1, GK_STORED = 2, GK_SHDR = 3, GK_FINAL = 4 };
+struct GenState {
+  uint64_t pos;     // bit position relative to `in`
+  uint64_t hdr;     // GK_HUFF: bit position of the block's header
+  uint32_t kind;    // GK_*: a block start, a token start inside a Huffman body,
+                    // a byte inside a stored payload, a stored LEN field, the end
+  uint32_t rem;     // GK_STORED: payload bytes left
+  uint32_t bfinal;  // GK_STORED / GK_SHDR: the block is the last one
+  uint32_t pad;
+};
+struct GenJob {
+  GenState st;       // start state
+  uint64_t stop;     // the unit ends at the first block / token / payload byte at or after this bit (~0: none)
+  uint64_t tok_off;  // token slot
+  uint32_t tok_cap;
+  uint32_t spec;     // guessed start: record the path's first token starts
+};
+struct GenResult {
+  GenState end;        // state where the unit stopped (GK_FINAL: the stream ended)
+  uint64_t out_len;    // bytes its tokens produce
+  uint64_t dec_start;  // bit where the recorded token path starts
+  uint64_t tab_id;     // tables of that path: its block's header position, or kFixedHdr
+  uint64_t out_stop;   // bytes of the tokens before the end state
+  uint32_t ntok;       // tokens, including the overlap decoded past the end state
+  uint32_t ntok_stop;  // tokens before the end state
+  int32_t status;
+  int32_t detail;
+  uint32_t recorded;   // the token-start bitmap of the first round is valid
+  uint32_t tab_final;  // BFINAL of that path's block
+  uint32_t tail_ok;    // an overlap past a GK_HUFF end state was decoded (its token starts recorded)
+  uint32_t pad;
+};
+// GenState::hdr of a fixed-code block: every fixed block has the same tables
+constexpr uint64_t kFixedHdr = 1ull << 62;
+struct GenLink {       // unit k against unit k-1's end state
+  uint64_t bytes;      // output bytes of unit k's tokens before the join
+  uint64_t prev_bytes; // output bytes of unit k-1's tokens before the join
+  uint32_t ok;         // 1: unit k continues unit k-1's path
+  uint32_t t;          // unit k's first token on the joint path
+  uint32_t prev_cut;   // unit k-1's tokens before the join
+  uint32_t pad;
+};
+struct GenSeg {        // copy segment of the general path
+  uint64_t base16;     // its u16 output (byte or window marker) in the staging array
+  uint64_t out_off;    // final output offset
+  uint64_t len;
+};
+int inflate_general_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t index, uint8_t **d_out_io,
+                        size_t out_cap, size_t *out_len, size_t *end_ip, hipStream_t s);
 
 int inflate_jobs_dev(const InfJob *d_jobs, InfResult *d_res, int count, hipStream_t s);
 int inflate_error(int status, int detail);

@@ -37,7 +37,8 @@ class KernelTimes(ctypes.Structure):
     _fields_ = [("deflate_ms", ctypes.c_double), ("deflate_launches", ctypes.c_uint64),
                 ("inflate_ms", ctypes.c_double), ("inflate_launches", ctypes.c_uint64),
                 ("deflate_pipeline_ms", ctypes.c_double), ("deflate_pipelines", ctypes.c_uint64),
-                ("inflate_tok_ms", ctypes.c_double), ("inflate_toks", ctypes.c_uint64)]
+                ("inflate_tok_ms", ctypes.c_double), ("inflate_toks", ctypes.c_uint64),
+                ("inflate_paths", ctypes.c_uint64 * 3), ("general_passes", ctypes.c_uint64)]
 
 
 class InflateOpts(ctypes.Structure):
@@ -75,6 +76,7 @@ def _load():
     sig = {
         "zt_device_count": ([], ctypes.c_int),
         "zt_set_device": ([ctypes.c_int], ctypes.c_int),
+        "zt_set_devices": ([ctypes.c_uint64], ctypes.c_int),
         "zt_last_error_message": ([], ctypes.c_char_p),
         "zt_version": ([], ctypes.c_char_p),
         "zt_free": ([vp], None),
@@ -87,6 +89,8 @@ def _load():
                                  ctypes.c_int),
         "zt_deflate_raw_batch": ([P(vp), P(sz), sz, P(DeflateOpts), u8pp, P(sz), P(ctypes.c_int)], ctypes.c_int),
         "zt_gzip_compress": ([vp, sz, P(GzipOpts), u8pp, P(sz), P(u32)], ctypes.c_int),
+        "zt_gzip_compress_batch": ([P(vp), P(sz), sz, P(GzipOpts), u8pp, P(sz), P(ctypes.c_int)], ctypes.c_int),
+        "zt_zlib_compress_batch": ([P(vp), P(sz), sz, P(DeflateOpts), u8pp, P(sz), P(ctypes.c_int)], ctypes.c_int),
         "zt_gunzip": ([vp, sz, u8pp, P(sz), P(P(GzipMember)), P(sz)], ctypes.c_int),
         "zt_zlib_compress": ([vp, sz, P(DeflateOpts), u8pp, P(sz), P(u32)], ctypes.c_int),
         "zt_zlib_decompress": ([vp, sz, sz, ctypes.c_int, u8pp, P(sz), P(sz), P(u32)], ctypes.c_int),
@@ -116,9 +120,9 @@ lib = _load()
 
 # every symbol include/zt.h declares (checked by tests/test_abi.py)
 SYMBOLS = [
-    "zt_device_count", "zt_set_device", "zt_last_error_message", "zt_version", "zt_free", "zt_crc32_update",
+    "zt_device_count", "zt_set_device", "zt_set_devices", "zt_last_error_message", "zt_version", "zt_free", "zt_crc32_update",
     "zt_adler32_update", "zt_checksums", "zt_deflate_raw", "zt_inflate_raw", "zt_inflate_raw_batch",
-    "zt_deflate_raw_batch", "zt_gzip_compress", "zt_gunzip", "zt_zlib_compress", "zt_zlib_decompress",
+    "zt_deflate_raw_batch", "zt_gzip_compress", "zt_gzip_compress_batch", "zt_zlib_compress_batch", "zt_gunzip", "zt_zlib_compress", "zt_zlib_decompress",
     "zt_dev_checksums", "zt_deflate_plan_create", "zt_deflate_plan_destroy",
     "zt_deflate_bound", "zt_deflate_dev", "zt_inflate_plan_create", "zt_inflate_plan_destroy", "zt_inflate_dev",
     "zt_synth_dev", "zt_synth_dev_at", "zt_timing_enable", "zt_timing_read",
@@ -137,6 +141,11 @@ def _cbuf(data):
 
 def device_count():
     return lib.zt_device_count()
+
+
+def set_devices(mask):
+    """Devices the batch calls split over (bit d = device d; 0 = this thread's)."""
+    _check(lib.zt_set_devices(mask))
 
 
 def set_device(d):
@@ -253,6 +262,52 @@ def gzip_compress(data, name=None, comment=None, hcrc=False, mtime=0, compressio
     crc = ctypes.c_uint32()
     _check(lib.zt_gzip_compress(b, n, ctypes.byref(o), ctypes.byref(out), ctypes.byref(olen), ctypes.byref(crc)))
     return _take(out, olen), crc.value
+
+
+def _batch_ptrs(items):
+    bs = [bytes(x) for x in items]
+    k = len(bs)
+    ptrs = (ctypes.c_void_p * k)(*[ctypes.cast(ctypes.c_char_p(x), ctypes.c_void_p).value for x in bs])
+    lens = (ctypes.c_size_t * k)(*[len(x) for x in bs])
+    return bs, ptrs, lens
+
+
+def _batch_take(k, outs, olens):
+    res = []
+    for i in range(k):
+        res.append(ctypes.string_at(outs[i], olens[i]) if outs[i] else b"")
+        if outs[i]:
+            lib.zt_free(outs[i])
+    return res
+
+
+def gzip_compress_batch(items, name=None, comment=None, hcrc=False, mtime=0, compression_type=2, lazy=0, level=-1):
+    """GZip members of many buffers in one pipeline per device (config C4)."""
+    bs, ptrs, lens = _batch_ptrs(items)
+    k = len(bs)
+    o = GzipOpts()
+    o.deflate = DeflateOpts(compression_type, lazy, level)
+    o.fname, o.fcomment, o.fhcrc, o.mtime = int(name is not None), int(comment is not None), int(hcrc), mtime
+    if name is not None:
+        o.name, o.name_len = bytes(name), len(name)
+    if comment is not None:
+        o.comment, o.comment_len = bytes(comment), len(comment)
+    outs = (ctypes.POINTER(ctypes.c_uint8) * k)()
+    olens = (ctypes.c_size_t * k)()
+    st = (ctypes.c_int * k)()
+    _check(lib.zt_gzip_compress_batch(ptrs, lens, k, ctypes.byref(o), outs, olens, st))
+    return _batch_take(k, outs, olens)
+
+
+def zlib_compress_batch(items, compression_type=2, lazy=0, level=-1):
+    bs, ptrs, lens = _batch_ptrs(items)
+    k = len(bs)
+    opts = DeflateOpts(compression_type, lazy, level)
+    outs = (ctypes.POINTER(ctypes.c_uint8) * k)()
+    olens = (ctypes.c_size_t * k)()
+    st = (ctypes.c_int * k)()
+    _check(lib.zt_zlib_compress_batch(ptrs, lens, k, ctypes.byref(opts), outs, olens, st))
+    return _batch_take(k, outs, olens)
 
 
 def gunzip(data):
@@ -376,4 +431,5 @@ def timing_read():
     return {"deflate_ms": t.deflate_ms, "deflate_launches": t.deflate_launches,
             "inflate_ms": t.inflate_ms, "inflate_launches": t.inflate_launches,
             "deflate_pipeline_ms": t.deflate_pipeline_ms, "deflate_pipelines": t.deflate_pipelines,
-            "inflate_tok_ms": t.inflate_tok_ms, "inflate_toks": t.inflate_toks}
+            "inflate_tok_ms": t.inflate_tok_ms, "inflate_toks": t.inflate_toks,
+            "inflate_paths": list(t.inflate_paths), "general_passes": t.general_passes}
