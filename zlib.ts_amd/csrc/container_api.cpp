@@ -53,7 +53,7 @@ int deflate_with_checksums(const uint8_t *in, size_t n, const zt_deflate_opts *o
   const size_t ss = deflate_scratch_bytes(c, n);
   ZT_TRY(scratch(c, 3, ss, &d_scr));
   ZT_TRY(scratch(c, 2, 16, &d_res));
-  if (n) ZT_HIP(hipMemcpyAsync(d_in, in, n, hipMemcpyHostToDevice, c->stream));
+  ZT_TRY(upload(c, d_in, in, n, c->stream));
   // the checksums run on the second stream beside the deflate pipeline (both
   // only read the input); every return below waits for that stream first
   uint32_t sums[2] = {0, 1};  // CRC-32 and Adler-32 of nothing
@@ -73,9 +73,11 @@ int deflate_with_checksums(const uint8_t *in, size_t n, const zt_deflate_opts *o
   uint8_t *h = (uint8_t *)malloc(prefix_len + len + trailer + 1);
   if (!h) return set_error(ZT_E_NOMEM, "host allocation failed");
   if (prefix_len) memcpy(h, prefix, prefix_len);
-  if (len) ZT_HIP(hipMemcpyAsync(h + prefix_len, d_out, len, hipMemcpyDeviceToHost, c->stream));
-  hipError_t e = hipStreamSynchronize(c->stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(c->aux);
+  if (const int rc = download(c, h + prefix_len, d_out, len, c->stream)) {
+    free(h);
+    return rc;
+  }
+  hipError_t e = hipStreamSynchronize(c->aux);
   if (e != hipSuccess) {
     free(h);
     return hip_fail(e, "hipStreamSynchronize");
@@ -178,6 +180,15 @@ int zt_gunzip(const uint8_t *in, size_t n, uint8_t **out, size_t *out_len, zt_gz
   std::vector<uint8_t> data;
   size_t ip = 0;
   char msg[128];
+  // the input goes to the device once; every member decodes from there
+  DeviceCtx *c;
+  ZT_TRY(get_ctx(&c));
+  std::lock_guard<std::recursive_mutex> ctx_lock(c->mu);
+  void *d_in = nullptr;
+  if (n) {
+    ZT_TRY(scratch(c, 19, n + 64, &d_in));
+    ZT_TRY(upload(c, d_in, in, n, c->stream));
+  }
   // src/GUnzip.ts:57-65: members until the input is consumed
   while (ip < n) {
     zt_gzip_member m;
@@ -232,7 +243,7 @@ int zt_gunzip(const uint8_t *in, size_t n, uint8_t **out, size_t *out_len, zt_gz
     // body (src/GUnzip.ts:149-153): the engine's RawInflate from index b.p
     uint8_t *o = nullptr;
     size_t olen = 0, eip = 0;
-    ZT_TRY(zt_inflate_raw(in, n, b.p, nullptr, &o, &olen, &eip));
+    ZT_TRY(inflate_dev_member(c, (const uint8_t *)d_in, n, b.p, &o, &olen, &eip));
     uint32_t crc = 0;
     const int rc = zt_crc32_update(0, o, olen, &crc);
     if (rc) {

@@ -88,6 +88,7 @@ int zt_deflate_dev(zt_deflate_plan *plan, const void *d_in, size_t n, size_t hal
   DeviceCtx *c;
   ZT_TRY(get_ctx(&c));
   std::lock_guard<std::recursive_mutex> ctx_lock(c->mu);
+  if (plan->device != c->device) return set_error(ZT_E_ARG, "plan belongs to another device (zt_set_device)");
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   if (halo > 32768) halo = 32768;
   return deflate_dev_run(c, (const uint8_t *)d_in, n, halo, final_, plan->ctype, plan->level, (uint8_t *)d_out,
@@ -108,13 +109,16 @@ int zt_deflate_raw(const uint8_t *in, size_t n, const zt_deflate_opts *opts, uin
   ZT_TRY(scratch(c, 1, ob, &d_out));
   const size_t ss = deflate_scratch_bytes(c, n);
   ZT_TRY(scratch(c, 3, ss, &d_scr));
-  if (n) ZT_HIP(hipMemcpyAsync(d_in, in, n, hipMemcpyHostToDevice, c->stream));
+  ZT_TRY(upload(c, d_in, in, n, c->stream));
   size_t len = 0;
   ZT_TRY(deflate_dev_run(c, (const uint8_t *)d_in, n, 0, 1, ct, lv, (uint8_t *)d_out, &len, d_scr, ss, c->stream));
   uint8_t *h = (uint8_t *)malloc(len ? len : 1);
   if (!h) return set_error(ZT_E_NOMEM, "host allocation failed");
-  ZT_HIP(hipMemcpyAsync(h, d_out, len, hipMemcpyDeviceToHost, c->stream));
-  ZT_HIP(hipStreamSynchronize(c->stream));
+  const int rc = download(c, h, d_out, len, c->stream);
+  if (rc) {
+    free(h);
+    return rc;
+  }
   *out = h;
   *out_len = len;
   return ZT_OK;
@@ -150,6 +154,7 @@ int zt_inflate_dev(zt_inflate_plan *plan, const void *d_in, size_t n, void *d_ou
   DeviceCtx *c;
   ZT_TRY(get_ctx(&c));
   std::lock_guard<std::recursive_mutex> ctx_lock(c->mu);
+  if (plan->device != c->device) return set_error(ZT_E_ARG, "plan belongs to another device (zt_set_device)");
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   uint8_t *o = (uint8_t *)d_out;
   size_t ol = 0, eip = 0;

@@ -170,35 +170,20 @@ static int batch_two_phase(DeviceCtx *c, const uint8_t *d_in, const std::vector<
   return ZT_OK;
 }
 
-// Decode `count` host streams; outputs are malloc'd.
-static int inflate_host_batch(const uint8_t *const *in, const size_t *n, const size_t *index, size_t count,
-                              const zt_inflate_opts *opts, uint8_t **out, size_t *out_len, size_t *end_ip,
-                              int *status) {
-  DeviceCtx *c;
-  ZT_TRY(get_ctx(&c));
-  std::lock_guard<std::recursive_mutex> ctx_lock(c->mu);
-  const int strict = opts ? opts->ref_strict : 0;
-  std::vector<size_t> in_off(count), cap(count);
-  size_t in_total = 0;
+// Decode `count` device-resident streams (stream i at d_in + in_off[i],
+// n[i] bytes, from index[i]); outputs are malloc'd.
+static int inflate_dev_batch(DeviceCtx *c, const void *d_in, const std::vector<size_t> &in_off, const size_t *n,
+                             const size_t *index, size_t count, int strict, uint8_t **out, size_t *out_len,
+                             size_t *end_ip, int *status) {
+  std::vector<size_t> cap(count);
   for (size_t i = 0; i < count; ++i) {
-    in_off[i] = in_total;
-    in_total += align_up(n[i] ? n[i] : 1, 256);
     // first guess; exact sizes are known after one pass
     size_t g = n[i] * 4;
     cap[i] = g < 65536 ? 65536 : g;
   }
-  void *d_in, *d_jobs, *d_res;
-  ZT_TRY(scratch(c, 0, in_total, &d_in));
+  void *d_jobs, *d_res;
   ZT_TRY(scratch(c, 2, count * (sizeof(InfJob) + sizeof(InfResult)) + 256, &d_jobs));
   d_res = (uint8_t *)d_jobs + align_up(count * sizeof(InfJob), 256);
-  // inputs packed into pinned staging, one H2D copy
-  {
-    void *h;
-    ZT_TRY(pinned(c, in_total, &h));
-    uint8_t *stage = (uint8_t *)h;
-    parallel_copy(count, [&](size_t i) { if (n[i]) memcpy(stage + in_off[i], in[i], n[i]); }, in_total);
-    ZT_HIP(hipMemcpyAsync(d_in, stage, in_total, hipMemcpyHostToDevice, c->stream));
-  }
   std::vector<InfJob> jobs(count);
   std::vector<InfResult> res(count);
   std::vector<size_t> todo;
@@ -213,6 +198,7 @@ static int inflate_host_batch(const uint8_t *const *in, const size_t *n, const s
     for (size_t i = 0; i < count; ++i) todo[i] = i;
   }
   for (int pass = 0; pass < 2 && !todo.empty(); ++pass) {
+    // (one wave per stream)
     size_t out_total = 0;
     std::vector<size_t> out_off(todo.size());
     for (size_t k = 0; k < todo.size(); ++k) {
@@ -281,6 +267,69 @@ static int inflate_host_batch(const uint8_t *const *in, const size_t *n, const s
   return first;
 }
 
+// Decode `count` host streams; outputs are malloc'd.
+static int inflate_host_batch(const uint8_t *const *in, const size_t *n, const size_t *index, size_t count,
+                              const zt_inflate_opts *opts, uint8_t **out, size_t *out_len, size_t *end_ip,
+                              int *status) {
+  DeviceCtx *c;
+  ZT_TRY(get_ctx(&c));
+  std::lock_guard<std::recursive_mutex> ctx_lock(c->mu);
+  const int strict = opts ? opts->ref_strict : 0;
+  std::vector<size_t> in_off(count);
+  size_t in_total = 0;
+  for (size_t i = 0; i < count; ++i) {
+    in_off[i] = in_total;
+    in_total += align_up(n[i] ? n[i] : 1, 256);
+  }
+  void *d_in;
+  ZT_TRY(scratch(c, 0, in_total, &d_in));
+  // inputs packed into pinned staging, one H2D copy
+  {
+    void *h;
+    ZT_TRY(pinned(c, in_total, &h));
+    uint8_t *stage = (uint8_t *)h;
+    parallel_copy(count, [&](size_t i) { if (n[i]) memcpy(stage + in_off[i], in[i], n[i]); }, in_total);
+    ZT_HIP(hipMemcpyAsync(d_in, stage, in_total, hipMemcpyHostToDevice, c->stream));
+  }
+  return inflate_dev_batch(c, d_in, in_off, n, index, count, strict, out, out_len, end_ip, status);
+}
+
+// One device-resident stream from `index` (gzip / zlib members): the
+// segment-parallel and general paths scan a window that grows 8x at a time
+// (a member's decode never scans the members after it, so many small members
+// stay linear), then the one-wave decoder.  Output malloc'd.
+int inflate_dev_member(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t index, uint8_t **out, size_t *out_len,
+                       size_t *end_ip) {
+  hipStream_t s = c->stream;
+  if (n >= index + (1u << 14)) {
+    for (size_t w = 4u << 20;; w *= 8) {
+      const size_t ne = std::min(n, index + w);
+      uint8_t *d_out = nullptr;
+      size_t ol = 0, eip = 0;
+      int seg = inflate_segments_dev(c, d_in, ne, index, &d_out, 0, &ol, &eip, s);
+      if (seg == 1) seg = inflate_general_dev(c, d_in, ne, index, &d_out, 0, &ol, &eip, s);
+      if (seg < 0) return seg;
+      if (seg == 0) {
+        uint8_t *h = (uint8_t *)malloc(ol ? ol : 1);
+        if (!h) return set_error(ZT_E_NOMEM, "host allocation failed");
+        const int rc = download(c, h, d_out, ol, s);
+        if (rc) {
+          free(h);
+          return rc;
+        }
+        *out = h;
+        *out_len = ol;
+        *end_ip = eip;
+        return ZT_OK;
+      }
+      if (ne == n) break;
+    }
+  }
+  std::vector<size_t> in_off(1, 0);
+  int st = 0;
+  return inflate_dev_batch(c, d_in, in_off, &n, &index, 1, 0, out, out_len, end_ip, &st);
+}
+
 }  // namespace zt
 
 using namespace zt;
@@ -297,7 +346,7 @@ int zt_inflate_raw(const uint8_t *in, size_t n, size_t index, const zt_inflate_o
     std::lock_guard<std::recursive_mutex> ctx_lock(c->mu);
     void *d_in;
     ZT_TRY(scratch(c, 0, n, &d_in));
-    ZT_HIP(hipMemcpyAsync(d_in, in, n, hipMemcpyHostToDevice, c->stream));
+    ZT_TRY(upload(c, d_in, in, n, c->stream));
     uint8_t *d_out = nullptr;
     size_t ol = 0, eip = 0;
     int seg = inflate_segments_dev(c, (const uint8_t *)d_in, n, index, &d_out, 0, &ol, &eip, c->stream);
@@ -307,8 +356,11 @@ int zt_inflate_raw(const uint8_t *in, size_t n, size_t index, const zt_inflate_o
     if (seg == 0) {
       uint8_t *h = (uint8_t *)malloc(ol ? ol : 1);
       if (!h) return set_error(ZT_E_NOMEM, "host allocation failed");
-      if (ol) ZT_HIP(hipMemcpyAsync(h, d_out, ol, hipMemcpyDeviceToHost, c->stream));
-      ZT_HIP(hipStreamSynchronize(c->stream));
+      const int rc = download(c, h, d_out, ol, c->stream);
+      if (rc) {
+        free(h);
+        return rc;
+      }
       *out = h;
       *out_len = ol;
       if (end_ip) *end_ip = eip;

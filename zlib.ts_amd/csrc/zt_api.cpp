@@ -2,6 +2,7 @@
 //
 // Every entry point computes on the GPU.  There is deliberately no CPU
 // fallback: without a HIP device the calls fail with ZT_E_NO_DEVICE.
+#include <algorithm>
 #include <functional>
 #include <thread>
 #include <cstdio>
@@ -122,6 +123,82 @@ int pinned(DeviceCtx *c, size_t bytes, void **ptr, int slot) {
   return ZT_OK;
 }
 
+// Large host buffers move through two pinned 32 MiB chunks: the host copy of
+// chunk k + 1 (a few threads) overlaps the DMA of chunk k -- pageable
+// hipMemcpy stages through the runtime's own small buffers at a fraction of
+// the PCIe rate.  Buffers below 8 MiB are copied directly.
+static constexpr size_t kXferChunk = 32u << 20;
+
+static void host_copy(void *dst, const void *src, size_t n) {
+  const size_t nt = n >= (8u << 20) ? 4 : 1;
+  if (nt == 1) {
+    memcpy(dst, src, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  const size_t per = (n + nt - 1) / nt;
+  for (size_t t = 0; t < nt; ++t) {
+    const size_t a = t * per, b = std::min(n, a + per);
+    if (a < b) th.emplace_back([=] { memcpy((uint8_t *)dst + a, (const uint8_t *)src + a, b - a); });
+  }
+  for (auto &t : th) t.join();
+}
+
+static int xfer_setup(DeviceCtx *c, uint8_t **buf) {
+  for (int k = 0; k < 2; ++k) {
+    void *p;
+    ZT_TRY(pinned(c, kXferChunk, &p, 2 + k));
+    buf[k] = static_cast<uint8_t *>(p);
+    if (!c->xfer_ev[k]) ZT_HIP(hipEventCreateWithFlags(&c->xfer_ev[k], hipEventDisableTiming));
+  }
+  return ZT_OK;
+}
+
+int upload(DeviceCtx *c, void *d_dst, const void *h_src, size_t n, hipStream_t s) {
+  if (n < (8u << 20)) {
+    if (n) ZT_HIP(hipMemcpyAsync(d_dst, h_src, n, hipMemcpyHostToDevice, s));
+    return ZT_OK;
+  }
+  uint8_t *buf[2];
+  ZT_TRY(xfer_setup(c, buf));
+  for (size_t off = 0, k = 0; off < n; off += kXferChunk, ++k) {
+    const size_t len = std::min(kXferChunk, n - off);
+    if (k >= 2) ZT_HIP(hipEventSynchronize(c->xfer_ev[k & 1]));
+    host_copy(buf[k & 1], (const uint8_t *)h_src + off, len);
+    ZT_HIP(hipMemcpyAsync((uint8_t *)d_dst + off, buf[k & 1], len, hipMemcpyHostToDevice, s));
+    ZT_HIP(hipEventRecord(c->xfer_ev[k & 1], s));
+  }
+  // the staging chunks are reused by the next call: let the last copies land
+  ZT_HIP(hipEventSynchronize(c->xfer_ev[0]));
+  ZT_HIP(hipEventSynchronize(c->xfer_ev[1]));
+  return ZT_OK;
+}
+
+int download(DeviceCtx *c, void *h_dst, const void *d_src, size_t n, hipStream_t s) {
+  if (n < (8u << 20)) {
+    if (n) ZT_HIP(hipMemcpyAsync(h_dst, d_src, n, hipMemcpyDeviceToHost, s));
+    ZT_HIP(hipStreamSynchronize(s));
+    return ZT_OK;
+  }
+  uint8_t *buf[2];
+  ZT_TRY(xfer_setup(c, buf));
+  const size_t nch = (n + kXferChunk - 1) / kXferChunk;
+  auto issue = [&](size_t k) -> int {
+    const size_t off = k * kXferChunk, len = std::min(kXferChunk, n - off);
+    ZT_HIP(hipMemcpyAsync(buf[k & 1], (const uint8_t *)d_src + off, len, hipMemcpyDeviceToHost, s));
+    ZT_HIP(hipEventRecord(c->xfer_ev[k & 1], s));
+    return ZT_OK;
+  };
+  ZT_TRY(issue(0));
+  for (size_t k = 0; k < nch; ++k) {
+    if (k + 1 < nch) ZT_TRY(issue(k + 1));
+    ZT_HIP(hipEventSynchronize(c->xfer_ev[k & 1]));
+    const size_t off = k * kXferChunk, len = std::min(kXferChunk, n - off);
+    host_copy((uint8_t *)h_dst + off, buf[k & 1], len);
+  }
+  return ZT_OK;
+}
+
 void parallel_copy(size_t count, const std::function<void(size_t)> &fn, size_t total_bytes) {
   // host memcpy fan-out for the batch paths: one thread per ~8 MiB, at most 8
   size_t nt = total_bytes >> 23;
@@ -224,7 +301,7 @@ static int checksums_host(const uint8_t *data, size_t len, uint32_t crc_in, uint
   if (!data) return set_error(ZT_E_ARG, "null data");
   void *d;
   ZT_TRY(scratch(c, 0, len, &d));
-  ZT_HIP(hipMemcpyAsync(d, data, len, hipMemcpyHostToDevice, c->stream));
+  ZT_TRY(upload(c, d, data, len, c->stream));
   return zt_dev_checksums(d, len, crc_in, adler_in, crc_out, adler_out, c->stream);
 }
 

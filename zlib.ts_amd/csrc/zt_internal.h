@@ -49,12 +49,13 @@ struct DeviceCtx {
   // second stream: checksums run beside the deflate pipeline in the containers
   hipStream_t aux = nullptr;
   hipEvent_t aux_ev = nullptr;
-  void *h_pinned[2] = {};  // pinned host staging: 0 batch data, 1 inflate metadata
+  void *h_pinned[4] = {};  // pinned host staging: 0 batch data, 1 inflate metadata, 2-3 upload/download chunks
+  hipEvent_t xfer_ev[2] = {};  // upload / download: chunk buffer k's copy has finished
   // zt_timing_enable: HIP-event kernel timing
   bool timing = false;
   hipEvent_t ev[8] = {};  // [2k, 2k+1]: interval k (0 match, 1 deflate pipeline, 2 inflate)
   zt_kernel_times times = {};
-  size_t pinned_size[2] = {};
+  size_t pinned_size[4] = {};
 };
 
 // Records the begin / end event of interval k (0 or 1) when timing is on.
@@ -293,6 +294,14 @@ int inflate_general_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t inde
                         size_t out_cap, size_t *out_len, size_t *end_ip, hipStream_t s);
 
 int inflate_jobs_dev(const InfJob *d_jobs, InfResult *d_res, int count, hipStream_t s);
+// one device-resident stream from `index`, output malloc'd (inflate_api.cpp)
+int inflate_dev_member(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t index, uint8_t **out, size_t *out_len,
+                       size_t *end_ip);
+// host -> device copy of n bytes: large buffers through two pinned staging
+// chunks (parallel memcpy overlapped with the DMA), small ones directly
+int upload(DeviceCtx *c, void *d_dst, const void *h_src, size_t n, hipStream_t s);
+// device -> host, the same way; returns after the bytes are in h_dst
+int download(DeviceCtx *c, void *h_dst, const void *d_src, size_t n, hipStream_t s);
 int inflate_error(int status, int detail);
 
 }  // namespace zt
