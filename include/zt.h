@@ -42,6 +42,11 @@ extern "C" {
 #define ZT_E_ZLIB_FCHECK -41             /* Error('invalid fcheck flag:N')           src/Inflate.ts:52 */
 #define ZT_E_ZLIB_FDICT -42              /* Error('fdict flag is not supported')     src/Inflate.ts:57 */
 #define ZT_E_ZLIB_ADLER -43              /* Error('invalid adler-32 checksum')       src/Inflate.ts:88 */
+#define ZT_E_ZIP_FORMAT -50              /* Error('End of Central Directory Record not found' | 'invalid file
+                                            header signature' | 'invalid file header size' | 'invalid local
+                                            file header signature')  src/Unzip.ts:39,89,160,236 */
+#define ZT_E_ZIP_CRC -51                 /* Error('Incorrect crc: file=0x.., data=0x..')  src/Unzip.ts:296 */
+#define ZT_E_ZIP_ENCRYPTED -52           /* Error('encrypted: please set password')  src/Unzip.ts:266 (no ZipCrypto) */
 #define ZT_E_NO_DEVICE -100              /* no HIP device: the engine never falls back to the CPU */
 #define ZT_E_HIP -101                    /* HIP runtime failure (see message) */
 #define ZT_E_NOMEM -102
@@ -144,6 +149,49 @@ int zt_gzip_compress_batch(const uint8_t *const *in, const size_t *n, size_t cou
  * src/Deflate.ts:60-99 (CMF/FLG, raw DEFLATE, Adler-32). */
 int zt_zlib_compress_batch(const uint8_t *const *in, const size_t *n, size_t count, const zt_deflate_opts *opts,
                            uint8_t **out, size_t *out_len, int *status);
+
+/* CRC-32 (initial 0) of `count` host buffers in one batched kernel launch
+ * (CRC32.create per buffer, src/CRC32.ts:25-47). */
+int zt_crc32_batch(const uint8_t *const *in, const size_t *n, size_t count, uint32_t *crc_out);
+
+/* ---- Zip / Unzip (no ZipCrypto) ---------------------- */
+/* One Zip.addFile(input, filename, opts) (src/Zip.ts:80-108). */
+typedef struct {
+  const uint8_t *name;    /* filename bytes (stringToByteArray: charCode & 0xFF) */
+  size_t name_len;
+  const uint8_t *comment; /* file comment bytes, or NULL */
+  size_t comment_len;
+  int method;             /* ZipCompressionMethod: 8 DEFLATE (default), 0 STORE */
+  int os;                 /* ZipOperatingSystem of the central header (default MSDOS = 0) */
+  uint8_t mtime[4];       /* DOS time / date bytes exactly as src/Zip.ts:130-139 builds them */
+  zt_deflate_opts deflate;/* deflateOptions */
+} zt_zip_file;
+/* Replaces Zip.compress()  src/Zip.ts:117-372: local headers + data, central
+ * directory, end record, laid out as the reference does; all DEFLATE members
+ * in one batch pipeline, all CRC-32s batched on the device.  The reference's
+ * extraField (written with a zero length, src/Zip.ts:215) is not supported. */
+int zt_zip_compress(const uint8_t *const *in, const size_t *n, const zt_zip_file *files, size_t count,
+                    const uint8_t *comment, size_t comment_len, uint8_t **out, size_t *out_len);
+/* One entry of an archive (FileHeader + its data, src/Unzip.ts:64-130). */
+typedef struct {
+  size_t name_off, name_len;       /* filename bytes in the input */
+  size_t comment_off, comment_len; /* file comment bytes in the input */
+  size_t data_off, data_len;       /* decompressed data in the output */
+  size_t local_offset;             /* relative offset of the local header */
+  uint32_t version, os, need_version, flags, method, time, date;
+  uint32_t crc32, compressed_size, plain_size; /* central directory fields */
+  uint32_t local_crc32, local_method;          /* local header fields (what getFileData uses) */
+  uint32_t data_crc32;             /* CRC-32 of the decompressed data (computed on the GPU) */
+  int32_t status;                  /* 0, or what getFileData(i) throws; message in `message` */
+  char message[96];
+} zt_unzip_entry;
+/* Replaces new Unzip(input, {verify}) + getFilenames() + getFileData(i) for
+ * every i  src/Unzip.ts:150-342: the archive's entries are parsed with the
+ * reference's checks and inflated in one batch.  Archive-level errors return
+ * with nothing filled; otherwise *out (all entries' data) and *entries are
+ * filled and the first failing entry's status is returned (its message set). */
+int zt_unzip(const uint8_t *in, size_t n, int verify, uint8_t **out, size_t *out_len, zt_unzip_entry **entries,
+             size_t *count);
 
 /* One decoded member (GUnzipMember, src/GUnzip.ts:66-175).  Offsets index the
  * input buffer (name, comment) or the concatenated output (data). */

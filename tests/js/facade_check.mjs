@@ -1,7 +1,7 @@
 // Runs the JS facade (zlib.ts_amd/lib) over cases prepared by
 // tests/test_js_facade.py and prints one JSON result per case.
 import fs from 'fs';
-import { RawDeflate, RawInflate, CRC32, Adler32, GZip, GUnzip, Deflate, Inflate, deviceCount } from '../../zlib.ts_amd/lib/index.js';
+import { RawDeflate, RawInflate, CRC32, Adler32, GZip, GUnzip, Deflate, Inflate, Zip, Unzip, deviceCount } from '../../zlib.ts_amd/lib/index.js';
 
 const hex = (s) => Uint8Array.from(Buffer.from(s, 'hex'));
 const tohex = (a) => Buffer.from(a.buffer, a.byteOffset, a.length).toString('hex');
@@ -55,6 +55,21 @@ for (const c of cases) {
             const z = new Inflate(hex(c.in), c.opts || {});
             r.out = tohex(z.decompress());
             r.ip = z.ip;
+        } else if (c.op === 'zip') {
+            // c.files: [{fn, in (hex), opts}], c.date: local-time components
+            const z = new Zip(c.comment || []);
+            for (const f of c.files) z.addFile(hex(f.in), f.fn, Object.assign({}, f.opts, { date: new Date(...c.date) }));
+            r.out = tohex(z.compress());
+        } else if (c.op === 'unzip') {
+            const u = new Unzip(hex(c.in), { verify: !!c.verify });
+            r.names = u.getFilenames();
+            r.files = r.names.map((nm) => {
+                try {
+                    return { name: nm, out: tohex(u.decompress(nm)) };
+                } catch (e) {
+                    return { name: nm, error: { message: e.message } };
+                }
+            });
         }
     } catch (e) {
         r.error = typeof e === 'string' ? { string: e } : { message: e.message, status: e.ztStatus };

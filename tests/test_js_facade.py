@@ -184,3 +184,52 @@ def test_facade_containers(oracle):
             assert r["adler32"] == oracle.adler32(data)
         else:
             assert blob_matches(want["out"], out) and r["ip"] == want["ip"]
+
+
+@pytest.mark.gpu
+def test_facade_zip_unzip(oracle):
+    """Zip / Unzip classes (src/Zip.ts, src/Unzip.ts) against the reference's
+    own archives (tests/golden/zip.json): STORE-only archives byte-identical,
+    every archive read back with the reference's names, data and errors."""
+    import hashlib
+
+    from test_zip_fixtures import gen_spec
+
+    recs = load("zip.json")["records"]
+    cases, checks = [], []
+    for i, rec in enumerate(recs):
+        arch = blob_bytes(rec["output"] if rec["kind"] == "zip" else rec["archive"])
+        for v in (False, True):
+            cases.append({"id": f"u{i}{int(v)}", "op": "unzip", "in": arch.hex(), "verify": v})
+            checks.append(("unzip", f"u{i}{int(v)}", rec["unzip_verify" if v else "unzip"]))
+        if rec["kind"] == "zip":
+            files = [{"fn": f["fn"], "in": gen_spec(oracle, f["spec"]).hex(), "opts": f["opts"]}
+                     for f in rec["archive"]["files"]]
+            cases.append({"id": f"z{i}", "op": "zip", "files": files, "date": rec["date"],
+                          "comment": rec["archive"]["comment"]})
+            checks.append(("zip", f"z{i}", (rec, arch)))
+    res = run_cases(cases)
+    for kind, cid, want in checks:
+        r = res[cid]
+        if kind == "unzip":
+            if not want["ok"]:
+                assert r.get("error", {}).get("message") == want["error"]["message"], (cid, r)
+                continue
+            assert r["names"] == want["names"], (cid, r)
+            for f, w in zip(r["files"], want["files"]):
+                if w["ok"]:
+                    assert hashlib.sha256(bytes.fromhex(f["out"])).hexdigest() == w["out"]["sha256"], cid
+                else:
+                    assert f["error"]["message"] == w["error"]["message"], (cid, f)
+        else:
+            rec, ref = want
+            out = bytes.fromhex(r["out"])
+            if all(f["opts"].get("compressionMethod") == 0 for f in rec["archive"]["files"]):
+                assert out == ref, cid
+            else:
+                import io
+                import zipfile
+
+                with zipfile.ZipFile(io.BytesIO(out)) as zf:
+                    for f in rec["archive"]["files"]:
+                        assert zf.read(f["fn"]) == gen_spec(oracle, f["spec"])

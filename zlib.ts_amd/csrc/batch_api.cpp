@@ -266,6 +266,35 @@ int zt_gzip_compress_batch(const uint8_t *const *in, const size_t *n, size_t cou
   return run_batch(in, n, count, ct, lv, fr, out, out_len, status);
 }
 
+int zt_crc32_batch(const uint8_t *const *in, const size_t *n, size_t count, uint32_t *crc_out) {
+  if (count == 0) return ZT_OK;
+  if (!in || !n || !crc_out) return set_error(ZT_E_ARG, "null argument");
+  DeviceCtx *c;
+  ZT_TRY(get_ctx(&c));
+  std::lock_guard<std::recursive_mutex> ctx_lock(c->mu);
+  std::vector<uint64_t> off(count), len(count);
+  uint64_t tot = 0;
+  for (size_t i = 0; i < count; ++i) {
+    if (n[i] && !in[i]) return set_error(ZT_E_ARG, "null input");
+    off[i] = tot;
+    len[i] = n[i];
+    tot += (n[i] + 255) & ~uint64_t(255);
+  }
+  void *d_in, *h, *d_sums;
+  ZT_TRY(scratch(c, 0, tot + 64, &d_in));
+  ZT_TRY(pinned(c, tot + 64, &h, 0));
+  uint8_t *stage = static_cast<uint8_t *>(h);
+  parallel_copy(count, [&](size_t i) { if (n[i]) memcpy(stage + off[i], in[i], n[i]); }, tot);
+  ZT_HIP(hipMemcpyAsync(d_in, stage, tot ? tot : 1, hipMemcpyHostToDevice, c->stream));
+  ZT_TRY(scratch(c, 18, 8 * count, &d_sums));
+  ZT_TRY(checksums_batch_dev(c, (const uint8_t *)d_in, count, off.data(), len.data(), (uint32_t *)d_sums, c->stream));
+  std::vector<uint32_t> sums(2 * count);
+  ZT_HIP(hipMemcpyAsync(sums.data(), d_sums, 8 * count, hipMemcpyDeviceToHost, c->stream));
+  ZT_HIP(hipStreamSynchronize(c->stream));
+  for (size_t i = 0; i < count; ++i) crc_out[i] = sums[2 * i];
+  return ZT_OK;
+}
+
 int zt_zlib_compress_batch(const uint8_t *const *in, const size_t *n, size_t count, const zt_deflate_opts *opts,
                            uint8_t **out, size_t *out_len, int *status) {
   if (count == 0) return ZT_OK;

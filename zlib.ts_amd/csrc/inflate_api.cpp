@@ -61,7 +61,7 @@ static int batch_two_phase(DeviceCtx *c, const uint8_t *d_in, const std::vector<
     j.start = in_off[i] + (index ? index[i] : 0);
     j.end = in_off[i] + n[i];
     // tokens <= output bytes; every token takes >= 1 input bit
-    uint64_t cap = std::max<uint64_t>(65536, 4 * (uint64_t)n[i]);
+    uint64_t cap = std::max<uint64_t>(65536, 4 * (uint64_t)(n[i] - (index ? index[i] : 0)));
     cap = std::min<uint64_t>(cap, (j.end - j.start) * 8) + 64;
     cap = std::min<uint64_t>(cap, 1u << 30);
     j.tok_off = tok_total;
@@ -172,6 +172,9 @@ static int batch_two_phase(DeviceCtx *c, const uint8_t *d_in, const std::vector<
 
 // Decode `count` device-resident streams (stream i at d_in + in_off[i],
 // n[i] bytes, from index[i]); outputs are malloc'd.
+int inflate_batch_dev_streams(DeviceCtx *c, const void *d_in, const std::vector<size_t> &in_off, const size_t *n,
+                              const size_t *index, size_t count, uint8_t **out, size_t *out_len, size_t *end_ip,
+                              int *status);
 static int inflate_dev_batch(DeviceCtx *c, const void *d_in, const std::vector<size_t> &in_off, const size_t *n,
                              const size_t *index, size_t count, int strict, uint8_t **out, size_t *out_len,
                              size_t *end_ip, int *status) {
@@ -265,6 +268,12 @@ static int inflate_dev_batch(DeviceCtx *c, const void *d_in, const std::vector<s
     if (status[i] && first == ZT_OK) first = inflate_error(res[i].status, res[i].detail);
   }
   return first;
+}
+
+int inflate_batch_dev_streams(DeviceCtx *c, const void *d_in, const std::vector<size_t> &in_off, const size_t *n,
+                              const size_t *index, size_t count, uint8_t **out, size_t *out_len, size_t *end_ip,
+                              int *status) {
+  return inflate_dev_batch(c, d_in, in_off, n, index, count, 0, out, out_len, end_ip, status);
 }
 
 // Decode `count` host streams; outputs are malloc'd.

@@ -87,12 +87,12 @@ __device__ __forceinline__ uint32_t ldw(g_u32 *a32, int64_t wi, uint64_t lo, uin
 __global__ __launch_bounds__(256) void find_blocks(const uint8_t *in, uint64_t n, uint64_t index, uint64_t w_first,
                                                    uint64_t nw, uint64_t *listb, uint32_t *cntb, uint64_t *list,
                                                    uint32_t *cnt) {
+  // (every lane runs to the end: the appends are wave-aggregated)
   const uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (k >= nw) return;
   const uintptr_t a = reinterpret_cast<uintptr_t>(in);
   g_u32 *a32 = (g_u32 *)(a & ~uintptr_t(15));
   const uint64_t lo = a & 15, hi = lo + n;
-  const int64_t wi = (int64_t)(w_first + k);
+  const int64_t wi = (int64_t)(w_first + (k < nw ? k : nw));
   const uint32_t wm = ldw(a32, wi - 1, lo, hi);
   const uint32_t w0 = ldw(a32, wi, lo, hi), w1 = ldw(a32, wi + 1, lo, hi);
   const uint32_t w2 = ldw(a32, wi + 2, lo, hi), w3 = ldw(a32, wi + 3, lo, hi);
@@ -103,8 +103,10 @@ __global__ __launch_bounds__(256) void find_blocks(const uint8_t *in, uint64_t n
   const uint64_t base = (uint64_t)wi * 32;
   const uint64_t pmin = (lo + index) * 8;
   const uint64_t pmax = hi * 8 >= 17 ? hi * 8 - 17 : 0;  // a header needs >= 17 bits
+  if (k >= nw) M = 0;
   if (base < pmin) M = (pmin - base >= 32) ? 0u : (M & (0xFFFFFFFFu << (pmin - base)));
   if (base + 32 > pmax) M = (base >= pmax) ? 0u : (M & (0xFFFFFFFFu >> (32 - (pmax - base))));
+  uint32_t B = 0;  // survivors of stage B
   while (M) {
     const int j = __builtin_ctz(M);
     M &= M - 1;
@@ -119,16 +121,33 @@ __global__ __launch_bounds__(256) void find_blocks(const uint8_t *in, uint64_t n
       const uint32_t l = (uint32_t)(cl >> (3 * i)) & 7;
       kraft += (i < ncl && l) ? (128u >> l) : 0u;
     }
-    if (kraft == 128) {
-      const uint32_t q = atomicAdd(cntb, 1u);
-      if (q < kMaxCandB) listb[q] = base + j;
-    }
+    if (kraft == 128) B |= 1u << j;
+  }
+  // one atomic per wave: survivors appended at a wave-reserved range
+  const uint32_t nbk = __popc(B);
+  uint32_t pre = nbk;
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t v = __shfl_up(pre, off, 64);
+    if (lane >= off) pre += v;
+  }
+  const uint32_t wtot = __shfl(pre, 63, 64);
+  uint32_t wbase = 0;
+  if (lane == 63 && wtot) wbase = atomicAdd(cntb, wtot);
+  wbase = __shfl(wbase, 63, 64);
+  uint32_t q = wbase + pre - nbk;
+  while (B) {
+    const int j = __builtin_ctz(B);
+    B &= B - 1;
+    if (q < kMaxCandB) listb[q] = base + j;
+    ++q;
   }
   // stored LEN fields at bytes 4 wi + j
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const uint64_t q = (uint64_t)wi * 4 + j;
-    if (q < lo + index + 1 || q + 4 > hi) continue;
+    if (k >= nw || q < lo + index + 1 || q + 4 > hi) continue;
     const uint32_t x = j ? __builtin_amdgcn_alignbyte(w1, w0, j) : w0;
     const uint32_t prevb = j ? (w0 >> (8 * (j - 1))) & 0xFF : wm >> 24;
     if (((x ^ (x >> 16)) & 0xFFFF) == 0xFFFF && (prevb >> 6) == 0) {
@@ -659,38 +678,86 @@ __global__ __launch_bounds__(64) void copy_marker_kernel(ResolveParams P, const 
 
 // The 32 KiB window after each segment, in order: window j = the last 32 KiB
 // of segment j with its markers looked up in window j - 1 (kept in LDS).
+// Thread t owns entries [32 t, 32 t + 32); the next segment's tail is loaded
+// while this one resolves, so a step costs its LDS lookups and one barrier.
+__device__ __forceinline__ void wc_load(const GenSeg *gs, uint32_t j, uint32_t nwin, const uint16_t *out16,
+                                        uint32_t tid, u32x4g *v) {
+  if (j >= nwin) return;
+  const GenSeg g = gs[j];
+  if (g.len < (uint64_t)RING) return;  // short segment: resolved entry by entry
+  const u32x4g *p = reinterpret_cast<const u32x4g *>(out16 + g.base16 + (g.len - RING) + 32 * tid);
+  const uintptr_t al = reinterpret_cast<uintptr_t>(p) & 15;
+  if (al == 0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = p[k];
+  } else {
+    const uint16_t *e = out16 + g.base16 + (g.len - RING) + 32 * tid;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v[k].x = e[8 * k] | ((uint32_t)e[8 * k + 1] << 16);
+      v[k].y = e[8 * k + 2] | ((uint32_t)e[8 * k + 3] << 16);
+      v[k].z = e[8 * k + 4] | ((uint32_t)e[8 * k + 5] << 16);
+      v[k].w = e[8 * k + 6] | ((uint32_t)e[8 * k + 7] << 16);
+    }
+  }
+}
+
 __global__ __launch_bounds__(1024) void window_chain_kernel(const GenSeg *gs, uint32_t nwin, const uint16_t *out16,
                                                             uint8_t *wins) {
-  __shared__ uint8_t w[2][RING];
+  __shared__ uint32_t w[2][RING / 4];
   const uint32_t tid = threadIdx.x;
+  u32x4g cur[4], nxt[4];
+  wc_load(gs, 0, nwin, out16, tid, cur);
   for (uint32_t j = 0; j < nwin; ++j) {
-    uint8_t *cur = w[j & 1];
-    const uint8_t *prv = w[(j & 1) ^ 1];
+    uint32_t *cw = w[j & 1];
+    const uint8_t *prv = reinterpret_cast<const uint8_t *>(w[(j & 1) ^ 1]);
+    wc_load(gs, j + 1, nwin, out16, tid, nxt);
     const GenSeg g = gs[j];
-    const uint16_t *src = out16 + g.base16;
+    uint32_t o[8];
     if (g.len >= (uint64_t)RING) {
-      const uint64_t b = g.len - RING;
-      for (uint32_t i = tid; i < (uint32_t)RING; i += 1024) {
-        const uint32_t x = src[b + i];
-        cur[i] = (uint8_t)((x & 0x8000u) ? prv[x & 0x7FFF] : x);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t e[4] = {cur[k].x, cur[k].y, cur[k].z, cur[k].w};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          uint32_t r = 0;
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            const uint32_t x = (e[2 * h + (b >> 1)] >> (16 * (b & 1))) & 0xFFFF;
+            const uint32_t v = (x & 0x8000u) ? prv[x & 0x7FFF] : x;
+            r |= (v & 0xFF) << (8 * b);
+          }
+          o[2 * k + h] = r;
+        }
       }
     } else {
-      for (uint32_t i = tid; i < (uint32_t)RING; i += 1024) {
-        const int64_t p = (int64_t)g.len - RING + i;
-        uint8_t v;
-        if (p >= 0) {
-          const uint32_t x = src[p];
-          v = (uint8_t)((x & 0x8000u) ? prv[x & 0x7FFF] : x);
-        } else {
-          v = j ? prv[i + g.len] : 0;
+      const uint16_t *src = out16 + g.base16;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        uint32_t r = 0;
+        for (int b = 0; b < 4; ++b) {
+          const uint32_t i = 32 * tid + 4 * q + b;
+          const int64_t p = (int64_t)g.len - RING + i;
+          uint32_t v;
+          if (p >= 0) {
+            const uint32_t x = src[p];
+            v = (x & 0x8000u) ? prv[x & 0x7FFF] : x;
+          } else {
+            v = j ? prv[i + g.len] : 0u;
+          }
+          r |= (v & 0xFF) << (8 * b);
         }
-        cur[i] = v;
+        o[q] = r;
       }
     }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) cw[8 * tid + q] = o[q];
+    u32x4g *gw = reinterpret_cast<u32x4g *>(wins + (uint64_t)j * RING + 32 * tid);
+    gw[0] = u32x4g{o[0], o[1], o[2], o[3]};
+    gw[1] = u32x4g{o[4], o[5], o[6], o[7]};
     __syncthreads();
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    for (uint32_t i = tid * 16; i < (uint32_t)RING; i += 1024 * 16)
-      *reinterpret_cast<u32x4 *>(wins + (uint64_t)j * RING + i) = *reinterpret_cast<const u32x4 *>(&cur[i]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
   }
 }
 
@@ -803,9 +870,10 @@ int inflate_general_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t inde
     cand.swap(keep);
   }
   // ---- 2. units on a grid of cells
-  uint64_t cell = ((bitn - bit0) / (8 * (uint64_t)std::max(c->num_cu, 1))) & ~uint64_t(7);
+  // cells: about 4 units per tokenize slot (8 per CU), 32 K .. 256 K bits
+  uint64_t cell = ((bitn - bit0) / (32 * (uint64_t)std::max(c->num_cu, 1))) & ~uint64_t(7);
   if (getenv("ZT_GEN_CELL")) cell = (uint64_t)atoll(getenv("ZT_GEN_CELL")) * 8;
-  cell = std::min<uint64_t>(std::max<uint64_t>(cell, 1u << 16), 1u << 18);
+  cell = std::min<uint64_t>(std::max<uint64_t>(cell, 1u << 15), 1u << 18);
   const uint64_t min_gap = 1u << 14;  // a unit spans at least this many bits (room for its successor to merge)
   std::vector<GenJob> jobs;
   std::vector<uint64_t> srcs;  // the candidate each guess came from (~0: exact start)
@@ -1033,7 +1101,12 @@ int inflate_general_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t inde
   std::vector<ChainUnit> chain;
   std::vector<SegJob> segs;
   std::vector<GenSeg> gsegs;
-  constexpr uint64_t kSeg = 1u << 20;
+  // copy segments: enough for two waves per CU, 128 KiB .. 1 MiB each
+  uint64_t out_est = 0;
+  for (size_t k = 0; k <= chain_end; ++k) out_est += res[k].out_stop;
+  uint64_t kSeg = std::min<uint64_t>(
+      1u << 20, std::max<uint64_t>(128u << 10, out_est / (2 * (uint64_t)std::max(c->num_cu, 1))));
+  if (getenv("ZT_GEN_SEG")) kSeg = std::max<uint64_t>(64u << 10, (uint64_t)atoll(getenv("ZT_GEN_SEG")));
   uint64_t total = 0, seg_start = 0, desc_total = 0, desc_seg = 0, base16 = 0;
   for (size_t k = 0; k <= chain_end; ++k) {
     // unit k's tokens [t, cut): from its join with k-1 to its join with k+1
@@ -1063,6 +1136,37 @@ int inflate_general_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t inde
   }
   gsegs.back().len = total - seg_start;
   base16 += al256(total - seg_start);
+  if (gen_debug()) {
+    fprintf(stderr, "[zt inflate gen] chain %zu units, %zu segments of ~%llu B, output %llu B\n", chain.size(),
+            gsegs.size(), (unsigned long long)kSeg, (unsigned long long)total);
+    if (getenv("ZT_GEN_TOKDUMP")) {
+      const size_t k = (size_t)atoll(getenv("ZT_GEN_TOKDUMP"));
+      for (size_t u = k - 1; u <= k && u < units; ++u) {
+        std::vector<uint32_t> tk(res[u].ntok);
+        ZT_HIP(hipMemcpy(tk.data(), gp.tokens + jobs[u].tok_off, tk.size() * 4, hipMemcpyDeviceToHost));
+        fprintf(stderr, "TOK unit %zu ntok_stop %u ntok %u:", u, res[u].ntok_stop, res[u].ntok);
+        const size_t a0 = u == k ? 0 : (res[u].ntok_stop > 20 ? res[u].ntok_stop - 20 : 0);
+        for (size_t i = a0; i < tk.size() && i < a0 + 120; ++i) fprintf(stderr, " %zu:%x", i, tk[i]);
+        fprintf(stderr, "\n");
+      }
+    }
+    if (getenv("ZT_GEN_DUMP")) {
+      for (size_t i = 0; i < chain.size(); ++i)
+        fprintf(stderr,
+                "  cu %zu out %llu len %u ntok %u | job kind %u pos %llu spec %u | t %u by %llu | cut %u cb %llu | "
+                "dec %llu end %u@%llu ntok %u/%u out %llu/%llu\n",
+                i, (unsigned long long)chain[i].out_off, chain[i].out_len, chain[i].ntok, jobs[i].st.kind,
+                (unsigned long long)jobs[i].st.pos, jobs[i].spec, i ? link[i].t : 0,
+                (unsigned long long)(i ? link[i].bytes : 0), i < chain_end ? link[i + 1].prev_cut : res[i].ntok_stop,
+                (unsigned long long)(i < chain_end ? link[i + 1].prev_bytes : res[i].out_stop),
+                (unsigned long long)res[i].dec_start, res[i].end.kind, (unsigned long long)res[i].end.pos,
+                res[i].ntok_stop, res[i].ntok, (unsigned long long)res[i].out_stop,
+                (unsigned long long)res[i].out_len);
+      for (size_t i = 0; i < gsegs.size(); ++i)
+        fprintf(stderr, "  seg %zu out %llu len %llu first %u count %u\n", i, (unsigned long long)gsegs[i].out_off,
+                (unsigned long long)gsegs[i].len, segs[i].first, segs[i].count);
+    }
+  }
   *out_len = total;
   *end_ip = (res[chain_end].end.pos + 7) >> 3;
   uint8_t *d_out = *d_out_io;

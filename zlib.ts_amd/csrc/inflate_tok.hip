@@ -197,6 +197,15 @@ __device__ __forceinline__ uint32_t tok_len(uint32_t t) { return (t >> 16) ? (t 
 //   whose source lies inside the step are resolved by pointer jumping.  The
 //   output goes through the ring to HBM in 8 KiB granules.
 
+// A descriptor copied from an earlier byte of the same copy step is used by a
+// later byte.  A ring read more than 32768 - CP_STEP back could then hit a slot
+// this step has already overwritten (a match chain reaching up to 32 KiB +
+// 255 back), so such a copy becomes an in-step reference to the byte it came
+// from, which copy_kernel resolves from the step itself.
+__device__ __forceinline__ uint32_t safe_desc(uint32_t d, uint32_t step_off) {
+  return ((d & 0x8000u) || d < 32768u - CP_STEP) ? d : (0x8100u | step_off);
+}
+
 struct ExpandShared {
   uint32_t tok[RS_TOK_RING];   // token chunks, filled by LDS-DMA
   uint32_t mark[64];
@@ -257,6 +266,7 @@ __global__ __launch_bounds__(64) void expand_kernel(ResolveParams P) {
     // by pointer jumping over the lanes)
     uint32_t dsc = 0x8000u;
     int32_t ptr = -1;
+    uint32_t first = 0;  // step offset of the byte's direct source
     if ((uint32_t)lane < W) {
       if ((tj >> 16) == 0) {
         dsc = 0x8000u | (tj & 0xFF);
@@ -276,12 +286,14 @@ __global__ __launch_bounds__(64) void expand_kernel(ResolveParams P) {
           else if (src < (int64_t)back)
             dsc = 0x8100u | (uint32_t)(src - (int64_t)ws);  // before this unit: copy_kernel resolves it
           else if (src < (int64_t)pos)
-            dsc = sh.cw[src - (int64_t)ws];  // an earlier window of this step, already resolved
+            dsc = safe_desc(sh.cw[src - (int64_t)ws], (uint32_t)(src - (int64_t)ws));  // an earlier window
           else
             ptr = (int32_t)(src - (int64_t)pos);
+          first = (uint32_t)(src - (int64_t)ws);
         }
       }
     }
+    const bool jumped = ptr >= 0;
     while (__ballot(ptr >= 0)) {
       const uint32_t q = ptr >= 0 ? (uint32_t)ptr : (uint32_t)lane;
       const uint32_t d2 = bperm(dsc, q);
@@ -295,6 +307,7 @@ __global__ __launch_bounds__(64) void expand_kernel(ResolveParams P) {
         }
       }
     }
+    if (jumped) dsc = safe_desc(dsc, first);
     if ((uint32_t)lane < W) {
       desc[op + lane] = (uint16_t)dsc;
       sh.cw[pos - ws + lane] = (uint16_t)dsc;

@@ -7,6 +7,8 @@ export { GZip, GZipFlagsMask, GZipMagicNumber, GZipOperatingSystem } from './GZi
 export { GUnzip } from './GUnzip.js';
 export { Deflate } from './Deflate.js';
 export { Inflate } from './Inflate.js';
+export { Zip, ZipCompressionMethod, ZipOperatingSystem, ZipFlags } from './Zip.js';
+export { Unzip } from './Unzip.js';
 import native from './native.js';
 export const deviceCount = () => native.deviceCount();
 export const version = () => native.version();

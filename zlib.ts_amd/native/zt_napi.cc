@@ -8,6 +8,7 @@
 
 #include <cstdio>
 #include <cstring>
+#include <vector>
 
 #include "../../include/zt.h"
 
@@ -304,6 +305,104 @@ napi_value zlib_decompress(napi_env env, napi_callback_info info) {
   return obj;
 }
 
+napi_value prop(napi_env env, napi_value obj, const char *k) {
+  napi_value v;
+  napi_get_named_property(env, obj, k, &v);
+  return v;
+}
+
+// zipCompress(files: [{data, name, comment (or null), method, os, mtime (4 bytes),
+//             compressionType, lazy, level}], comment: Uint8Array) -> Uint8Array
+napi_value zip_compress(napi_env env, napi_callback_info info) {
+  napi_value a[2];
+  args(env, info, a, 2);
+  uint32_t cnt = 0;
+  napi_get_array_length(env, a[0], &cnt);
+  std::vector<const uint8_t *> in(cnt);
+  std::vector<size_t> n(cnt);
+  std::vector<zt_zip_file> f(cnt);
+  for (uint32_t i = 0; i < cnt; ++i) {
+    napi_value e;
+    napi_get_element(env, a[0], i, &e);
+    memset(&f[i], 0, sizeof f[i]);
+    if (!get_u8(env, prop(env, e, "data"), &in[i], &n[i])) return nullptr;
+    if (!get_u8(env, prop(env, e, "name"), &f[i].name, &f[i].name_len)) return nullptr;
+    bool has = false;
+    if (!opt_u8(env, prop(env, e, "comment"), &f[i].comment, &f[i].comment_len, &has)) return nullptr;
+    f[i].method = (int)get_i64(env, prop(env, e, "method"), 8);
+    f[i].os = (int)get_i64(env, prop(env, e, "os"), 0);
+    const uint8_t *mt;
+    size_t ml;
+    if (!get_u8(env, prop(env, e, "mtime"), &mt, &ml)) return nullptr;
+    for (size_t k = 0; k < 4 && k < ml; ++k) f[i].mtime[k] = mt[k];
+    f[i].deflate.compression_type = (int)get_i64(env, prop(env, e, "compressionType"), 2);
+    f[i].deflate.lazy = (int)get_i64(env, prop(env, e, "lazy"), 0);
+    f[i].deflate.level = (int)get_i64(env, prop(env, e, "level"), -1);
+  }
+  const uint8_t *cm = nullptr;
+  size_t cl = 0;
+  bool has = false;
+  if (!opt_u8(env, a[1], &cm, &cl, &has)) return nullptr;
+  uint8_t *out = nullptr;
+  size_t olen = 0;
+  const int rc = zt_zip_compress(in.data(), n.data(), f.data(), cnt, cm, cl, &out, &olen);
+  if (rc) return throw_zt(env, rc);
+  return new_u8(env, out, olen);
+}
+
+// unzip(input, verify) -> {output, entries: [{nameOff, nameLen, ..., status, message}]}
+// (archive-level errors throw; an entry's error is in its status / message)
+napi_value unzip(napi_env env, napi_callback_info info) {
+  napi_value a[2];
+  args(env, info, a, 2);
+  const uint8_t *p;
+  size_t n;
+  if (!get_u8(env, a[0], &p, &n)) return nullptr;
+  bool verify = false;
+  napi_valuetype t;
+  napi_typeof(env, a[1], &t);
+  if (t == napi_boolean) napi_get_value_bool(env, a[1], &verify);
+  uint8_t *out = nullptr;
+  size_t olen = 0, cnt = 0;
+  zt_unzip_entry *ent = nullptr;
+  const int rc = zt_unzip(p, n, verify ? 1 : 0, &out, &olen, &ent, &cnt);
+  if (rc && !ent) return throw_zt(env, rc);
+  napi_value obj, arr;
+  napi_create_object(env, &obj);
+  napi_set_named_property(env, obj, "output", new_u8(env, out, olen));
+  napi_create_array_with_length(env, cnt, &arr);
+  for (size_t i = 0; i < cnt; ++i) {
+    const zt_unzip_entry &m = ent[i];
+    napi_value e;
+    napi_create_object(env, &e);
+    set_num(env, e, "nameOff", (double)m.name_off);
+    set_num(env, e, "nameLen", (double)m.name_len);
+    set_num(env, e, "commentOff", (double)m.comment_off);
+    set_num(env, e, "commentLen", (double)m.comment_len);
+    set_num(env, e, "dataOff", (double)m.data_off);
+    set_num(env, e, "dataLen", (double)m.data_len);
+    set_num(env, e, "relativeOffset", (double)m.local_offset);
+    set_num(env, e, "version", m.version);
+    set_num(env, e, "os", m.os);
+    set_num(env, e, "needVersion", m.need_version);
+    set_num(env, e, "flags", m.flags);
+    set_num(env, e, "compression", m.method);
+    set_num(env, e, "time", m.time);
+    set_num(env, e, "date", m.date);
+    set_num(env, e, "crc32", m.crc32);
+    set_num(env, e, "compressedSize", m.compressed_size);
+    set_num(env, e, "plainSize", m.plain_size);
+    set_num(env, e, "status", m.status);
+    napi_value msg;
+    napi_create_string_utf8(env, m.message, NAPI_AUTO_LENGTH, &msg);
+    napi_set_named_property(env, e, "message", msg);
+    napi_set_element(env, arr, (uint32_t)i, e);
+  }
+  zt_free(ent);
+  napi_set_named_property(env, obj, "entries", arr);
+  return obj;
+}
+
 napi_value device_count(napi_env env, napi_callback_info) {
   napi_value r;
   napi_create_int32(env, zt_device_count(), &r);
@@ -326,6 +425,8 @@ napi_value init(napi_env env, napi_value exports) {
       {"gunzip", nullptr, gunzip, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"zlibCompress", nullptr, zlib_compress, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"zlibDecompress", nullptr, zlib_decompress, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+      {"zipCompress", nullptr, zip_compress, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+      {"unzip", nullptr, unzip, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"deviceCount", nullptr, device_count, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"version", nullptr, version, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
   };

@@ -41,6 +41,22 @@ class KernelTimes(ctypes.Structure):
                 ("inflate_paths", ctypes.c_uint64 * 3), ("general_passes", ctypes.c_uint64)]
 
 
+class ZipFile(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char_p), ("name_len", ctypes.c_size_t), ("comment", ctypes.c_char_p),
+                ("comment_len", ctypes.c_size_t), ("method", ctypes.c_int), ("os", ctypes.c_int),
+                ("mtime", ctypes.c_uint8 * 4), ("deflate", DeflateOpts)]
+
+
+class UnzipEntry(ctypes.Structure):
+    _fields_ = [("name_off", ctypes.c_size_t), ("name_len", ctypes.c_size_t), ("comment_off", ctypes.c_size_t),
+                ("comment_len", ctypes.c_size_t), ("data_off", ctypes.c_size_t), ("data_len", ctypes.c_size_t),
+                ("local_offset", ctypes.c_size_t)] + [
+                    (f, ctypes.c_uint32) for f in ("version", "os", "need_version", "flags", "method", "time", "date",
+                                                   "crc32", "compressed_size", "plain_size", "local_crc32",
+                                                   "local_method", "data_crc32")] + [
+                    ("status", ctypes.c_int32), ("message", ctypes.c_char * 96)]
+
+
 class InflateOpts(ctypes.Structure):
     _fields_ = [("buffer_type", ctypes.c_int), ("buffer_size", ctypes.c_size_t), ("ref_strict", ctypes.c_int)]
 
@@ -91,6 +107,9 @@ def _load():
         "zt_gzip_compress": ([vp, sz, P(GzipOpts), u8pp, P(sz), P(u32)], ctypes.c_int),
         "zt_gzip_compress_batch": ([P(vp), P(sz), sz, P(GzipOpts), u8pp, P(sz), P(ctypes.c_int)], ctypes.c_int),
         "zt_zlib_compress_batch": ([P(vp), P(sz), sz, P(DeflateOpts), u8pp, P(sz), P(ctypes.c_int)], ctypes.c_int),
+        "zt_crc32_batch": ([P(vp), P(sz), sz, P(u32)], ctypes.c_int),
+        "zt_zip_compress": ([P(vp), P(sz), P(ZipFile), sz, vp, sz, u8pp, P(sz)], ctypes.c_int),
+        "zt_unzip": ([vp, sz, ctypes.c_int, u8pp, P(sz), P(P(UnzipEntry)), P(sz)], ctypes.c_int),
         "zt_gunzip": ([vp, sz, u8pp, P(sz), P(P(GzipMember)), P(sz)], ctypes.c_int),
         "zt_zlib_compress": ([vp, sz, P(DeflateOpts), u8pp, P(sz), P(u32)], ctypes.c_int),
         "zt_zlib_decompress": ([vp, sz, sz, ctypes.c_int, u8pp, P(sz), P(sz), P(u32)], ctypes.c_int),
@@ -122,7 +141,8 @@ lib = _load()
 SYMBOLS = [
     "zt_device_count", "zt_set_device", "zt_set_devices", "zt_last_error_message", "zt_version", "zt_free", "zt_crc32_update",
     "zt_adler32_update", "zt_checksums", "zt_deflate_raw", "zt_inflate_raw", "zt_inflate_raw_batch",
-    "zt_deflate_raw_batch", "zt_gzip_compress", "zt_gzip_compress_batch", "zt_zlib_compress_batch", "zt_gunzip", "zt_zlib_compress", "zt_zlib_decompress",
+    "zt_deflate_raw_batch", "zt_gzip_compress", "zt_gzip_compress_batch", "zt_zlib_compress_batch", "zt_gunzip",
+    "zt_crc32_batch", "zt_zip_compress", "zt_unzip", "zt_zlib_compress", "zt_zlib_decompress",
     "zt_dev_checksums", "zt_deflate_plan_create", "zt_deflate_plan_destroy",
     "zt_deflate_bound", "zt_deflate_dev", "zt_inflate_plan_create", "zt_inflate_plan_destroy", "zt_inflate_dev",
     "zt_synth_dev", "zt_synth_dev_at", "zt_timing_enable", "zt_timing_read",
@@ -308,6 +328,74 @@ def zlib_compress_batch(items, compression_type=2, lazy=0, level=-1):
     st = (ctypes.c_int * k)()
     _check(lib.zt_zlib_compress_batch(ptrs, lens, k, ctypes.byref(opts), outs, olens, st))
     return _batch_take(k, outs, olens)
+
+
+def crc32_batch(items):
+    bs, ptrs, lens = _batch_ptrs(items)
+    out = (ctypes.c_uint32 * len(bs))()
+    _check(lib.zt_crc32_batch(ptrs, lens, len(bs), out))
+    return list(out)
+
+
+def dos_mtime(year, month, day, hour, minute, second):
+    """The 4 DOS time / date bytes of src/Zip.ts:130-139 (month 1-12)."""
+    return bytes([((minute & 7) << 5) | (second >> 1), ((hour << 3) | (minute >> 3)) & 0xFF,
+                  ((month & 7) << 5) | day, (((year - 1980) & 0x7F) << 1) | (month >> 3)])
+
+
+def zip_compress(files, comment=b""):
+    """Zip.addFile(...) for each dict of `files` (data, name, comment, method,
+    os, mtime = 4 DOS bytes, compression_type, lazy) then Zip.compress()."""
+    k = len(files)
+    datas = [bytes(f["data"]) for f in files]
+    bs, ptrs, lens = _batch_ptrs(datas)
+    arr = (ZipFile * k)()
+    keep = []
+    for i, f in enumerate(files):
+        nm, cm = bytes(f.get("name", b"")), f.get("comment")
+        keep += [nm, cm]
+        arr[i].name, arr[i].name_len = nm, len(nm)
+        if cm is not None:
+            arr[i].comment, arr[i].comment_len = bytes(cm), len(cm)
+        arr[i].method = f.get("method", 8)
+        arr[i].os = f.get("os", 0)
+        arr[i].mtime = (ctypes.c_uint8 * 4)(*f.get("mtime", b"\0\0\0\0"))
+        arr[i].deflate = DeflateOpts(f.get("compression_type", 2), f.get("lazy", 0), f.get("level", -1))
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    olen = ctypes.c_size_t()
+    cb = bytes(comment)
+    _check(lib.zt_zip_compress(ptrs, lens, arr, k, cb, len(cb), ctypes.byref(out), ctypes.byref(olen)))
+    return _take(out, olen)
+
+
+def unzip(archive, verify=False):
+    """Unzip every entry.  Returns (first error or None, [entry dicts with
+    name, comment, data (or None), status, message and the header fields])."""
+    b, n = _cbuf(archive)
+    archive = bytes(archive)
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    olen = ctypes.c_size_t()
+    ents = ctypes.POINTER(UnzipEntry)()
+    cnt = ctypes.c_size_t()
+    rc = lib.zt_unzip(b, n, int(verify), ctypes.byref(out), ctypes.byref(olen), ctypes.byref(ents), ctypes.byref(cnt))
+    if rc != ZT_OK and not ents:
+        return ZtError(rc, lib.zt_last_error_message().decode(errors="replace")), []
+    data = ctypes.string_at(out, olen.value) if out else b""
+    res = []
+    for i in range(cnt.value):
+        e = ents[i]
+        d = {f: getattr(e, f) for f, _ in UnzipEntry._fields_ if f != "message"}
+        d["message"] = e.message.decode(errors="replace")
+        d["name"] = archive[e.name_off:e.name_off + e.name_len]
+        d["comment"] = archive[e.comment_off:e.comment_off + e.comment_len]
+        d["data"] = data[e.data_off:e.data_off + e.data_len] if e.status == 0 else None
+        res.append(d)
+    if out:
+        lib.zt_free(out)
+    if ents:
+        lib.zt_free(ents)
+    err = None if rc == ZT_OK else ZtError(rc, lib.zt_last_error_message().decode(errors="replace"))
+    return err, res
 
 
 def gunzip(data):
