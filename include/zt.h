@@ -51,6 +51,7 @@ extern "C" {
 #define ZT_E_HIP -101                    /* HIP runtime failure (see message) */
 #define ZT_E_NOMEM -102
 #define ZT_E_ARG -103
+#define ZT_E_INTERNAL -104               /* engine invariant broken (see message) */
 
 /* ---- devices ----------------------------------------------------------- */
 int zt_device_count(void);
@@ -107,6 +108,22 @@ typedef struct {
  * opts may be NULL. */
 int zt_inflate_raw(const uint8_t *in, size_t n, size_t index, const zt_inflate_opts *opts, uint8_t **out,
                    size_t *out_len, size_t *end_ip);
+
+/* Replaces RawInflateStream.decompress(input, ip)  src/RawInflateStream.ts:67-120
+ * (SURVEY.md 8(f) row 4): resumable decode of a stream that arrives in
+ * pieces.  Decodes from bit `bit_pos` of in[0..n) (bit k = bit k % 8 of byte
+ * k / 8), with window[0..wlen) -- the output already produced, of which the
+ * last 32 KiB are used -- as match history, every block that lies completely
+ * inside the input.  *out receives those blocks' bytes, *end_bits the bit
+ * position just after the last of them (resume there with more input),
+ * *finished 1 once the BFINAL block was decoded.  Running out of input is not
+ * an error (the output then ends at the last complete block); a corrupt
+ * stream fails with the reference's message (an error within the last 8
+ * bytes of the input counts as running out of input until more arrives).  The reference resumes at
+ * symbol granularity; this engine at block granularity: the concatenated
+ * output is identical. */
+int zt_inflate_raw_resume(const uint8_t *in, size_t n, uint64_t bit_pos, const uint8_t *window, size_t wlen,
+                          uint8_t **out, size_t *out_len, uint64_t *end_bits, int *finished);
 
 /* Batch forms: `count` independent buffers in one launch (config C2/C4).
  * status[i] receives each item's code; the call returns the first failure. */

@@ -1,7 +1,7 @@
 // Runs the JS facade (zlib.ts_amd/lib) over cases prepared by
 // tests/test_js_facade.py and prints one JSON result per case.
 import fs from 'fs';
-import { RawDeflate, RawInflate, CRC32, Adler32, GZip, GUnzip, Deflate, Inflate, Zip, Unzip, deviceCount } from '../../zlib.ts_amd/lib/index.js';
+import { RawDeflate, RawInflate, RawInflateStream, InflateStream, CRC32, Adler32, GZip, GUnzip, Deflate, Inflate, Zip, Unzip, deviceCount } from '../../zlib.ts_amd/lib/index.js';
 
 const hex = (s) => Uint8Array.from(Buffer.from(s, 'hex'));
 const tohex = (a) => Buffer.from(a.buffer, a.byteOffset, a.length).toString('hex');
@@ -60,6 +60,30 @@ for (const c of cases) {
             const z = new Zip(c.comment || []);
             for (const f of c.files) z.addFile(hex(f.in), f.fn, Object.assign({}, f.opts, { date: new Date(...c.date) }));
             r.out = tohex(z.compress());
+        } else if (c.op === 'rstream') {
+            // the stream arrives in pieces c.cuts (byte ends); every call is
+            // given the whole input received so far, as the reference's callers do
+            const all = hex(c.in);
+            const st = new RawInflateStream(all.subarray(0, 0), 0);
+            const parts = [];
+            for (const end of c.cuts) parts.push(st.decompress(all.subarray(0, end)));
+            r.out = parts.map(tohex).join('');
+            r.calls = parts.map((x) => x.length);
+            r.ip = st.ip;
+            r.bitpos = st.bitpos;
+            r.bfinal = st.bfinal;
+        } else if (c.op === 'zstream') {
+            // zlib stream in chunks appended by InflateStream.decompress(chunk)
+            const all = hex(c.in);
+            const st = new InflateStream(all.subarray(0, 0));
+            const parts = [];
+            let prev = 0;
+            for (const end of c.cuts) {
+                parts.push(st.decompress(all.subarray(prev, end)));
+                prev = end;
+            }
+            r.out = parts.map(tohex).join('');
+            r.checked = st.checked;
         } else if (c.op === 'unzip') {
             const u = new Unzip(hex(c.in), { verify: !!c.verify });
             r.names = u.getFilenames();

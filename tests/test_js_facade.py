@@ -233,3 +233,38 @@ def test_facade_zip_unzip(oracle):
                 with zipfile.ZipFile(io.BytesIO(out)) as zf:
                     for f in rec["archive"]["files"]:
                         assert zf.read(f["fn"]) == gen_spec(oracle, f["spec"])
+
+
+@pytest.mark.gpu
+def test_facade_inflate_streams(oracle):
+    """RawInflateStream / InflateStream (src/RawInflateStream.ts:67-120,
+    src/InflateStream.ts:29-57) fed in pieces: the concatenated output equals
+    the whole-stream decode, and the position ends past the stream."""
+    import random
+
+    rng = random.Random(7)
+    data = oracle.gen("wordsalad", 3, 300_000) + oracle.gen("xorshift32", 3, 40_000)
+    ref_stream, _ = oracle.raw_deflate(data)
+    zc = zlib.compressobj(6, zlib.DEFLATED, -15)
+    z_raw = zc.compress(data) + zc.flush()
+    cases = []
+    for name, s in [("ref", ref_stream), ("zlib", z_raw)]:
+        cuts = sorted(rng.sample(range(1, len(s)), 12)) + [len(s)]
+        cases.append({"id": name, "op": "rstream", "in": s.hex(), "cuts": cuts})
+    zs = zlib.compress(data, 6)
+    cuts = sorted(rng.sample(range(1, len(zs)), 9)) + [len(zs)]
+    cases.append({"id": "z", "op": "zstream", "in": zs.hex(), "cuts": cuts})
+    bad = bytearray(zs)
+    bad[-1] ^= 0xFF  # Adler-32 trailer
+    cases.append({"id": "zbad", "op": "zstream", "in": bytes(bad).hex(), "cuts": [len(bad) // 2, len(bad)]})
+    res = run_cases(cases)
+    for name, s in [("ref", ref_stream), ("zlib", z_raw)]:
+        r = res[name]
+        assert "error" not in r, r.get("error")
+        assert bytes.fromhex(r["out"]) == data, name
+        assert r["bfinal"] and (r["ip"] * 8 + r["bitpos"] + 7) // 8 == len(s), name
+    # zlib writes many blocks: the output arrives over several calls (the
+    # reference's RawDeflate writes one block, decoded once it is complete)
+    assert sum(1 for x in res["zlib"]["calls"] if x) >= 2
+    assert bytes.fromhex(res["z"]["out"]) == data and res["z"]["checked"]
+    assert res["zbad"]["error"]["message"] == "invalid adler-32 checksum"

@@ -328,6 +328,7 @@ __device__ __forceinline__ uint32_t near_any(const uint32_t (&w)[9], uint32_t cu
 // interleaved per thread so that their dependent LDS loads overlap.
 struct Walk {
   uint32_t p, q, link, max_len, best_len, best_dist, o, pw, omask, cur, cur2, cur3, cur4;
+  uint32_t cl;  // carried match length (kept unless the walk finds one at least as long, nearer)
   int hops, max_hops;
   bool active;
 };
@@ -365,6 +366,12 @@ __device__ __forceinline__ void walk_init(Walk &w, const MatchShared *s, const D
   w.hops = 0;
   w.max_hops = (int)w.best_len >= P.good ? (P.max_chain >> 2) : P.max_chain;
   w.active = w.max_len >= (uint32_t)P.klen && (int)w.best_len < P.skip_len;
+  w.cl = w.best_len;
+#ifdef ZT_DF_CARRY_TIES
+  // the walk visits the nearest candidates first: one as long as the carried
+  // match is found before the carried distance and costs fewer distance bits
+  if (w.best_len >= 4) w.best_len -= 1;
+#endif
   // one word per hop filters the candidates: the word ending at best_len (a
   // candidate can only win if it matches there), or before any match the
   // first bytes of the key (the chains' hash buckets also hold collisions)
@@ -461,7 +468,7 @@ template <int K>
 __device__ __forceinline__ uint32_t walk_finish(const Walk &w, const MatchShared *s, const DeflateParams &P,
                                                 const uint32_t (&win)[9], uint32_t near, uint32_t &carry_len,
                                                 uint32_t &carry_dist) {
-  uint32_t best_len = w.best_len, best_dist = w.best_dist;
+  uint32_t best_len = w.best_len < w.cl ? w.cl : w.best_len, best_dist = w.best_dist;
   // a far 3-byte match (carried from the previous position) is dropped in
   // the end: it must not hide a near one
   if (best_len == 3 && best_dist > (uint32_t)P.too_far) best_len = 0;
@@ -511,6 +518,9 @@ __device__ void search_quad(const MatchShared *s, const DeflateParams &P, uint32
   while (wa.active || wb.active) walk_pair_step(wa, wb, s, P);
   out[0] = walk_finish<0>(wa, s, P, w, nr0, c0l, c0d);
   out[2] = walk_finish<2>(wb, s, P, w, nr2, c2l, c2d);
+#ifdef ZT_DF_NOCARRY  // experiment: positions 1 and 3 start without the carried match
+  c0l = c0d = c2l = c2d = 0;
+#endif
   walk_init(wa, s, P, pb + 1, p1, win32<17>(w), win32<21>(w), win32<25>(w), win32<29>(w), c0l, c0d);
   walk_init(wb, s, P, pb + 3, p1, win32<19>(w), win32<23>(w), win32<27>(w), win32<31>(w), c2l, c2d);
   while (wa.active || wb.active) walk_pair_step(wa, wb, s, P);

@@ -225,11 +225,14 @@ __device__ __forceinline__ void inflate_stream(const InfJob &job, InfResult &res
   rd.init(job.in, job.n, job.start, sh->inbuf, lane);
   Writer wr;
   wr.ring = sh->ring;
-  wr.out = (g_out8 *)job.out;
-  wr.cap = job.cap;
-  wr.op = 0;
-  wr.flushed = 0;
+  // resume: the history is output position [0, hist_len), never written out
+  wr.out = (g_out8 *)(job.out - job.hist_len);
+  wr.cap = job.cap + job.hist_len;
+  wr.op = job.hist_len;
+  wr.flushed = job.hist_len;
   wr.lane = lane;
+  for (uint32_t i = lane; i < job.hist_len; i += 64) sh->ring[i & RING_MASK] = job.hist[i];
+  wave_sync();
   int status = ZT_OK, detail = 0;
   bool bfinal = false;
   int stop_idx = -1;
@@ -238,7 +241,11 @@ __device__ __forceinline__ void inflate_stream(const InfJob &job, InfResult &res
   uint32_t v;
 
   if (job.start > job.n) status = ZT_E_INPUT_BROKEN;
+  if (status == ZT_OK && job.start_bit && !rd.template bits<STRICT>((int)job.start_bit, v)) status = ZT_E_INPUT_BROKEN;
+  uint64_t blk_bits = job.start * 8 + job.start_bit, blk_op = wr.op;  // end of the last complete block
   while (status == ZT_OK && !bfinal) {
+    blk_bits = rd.pos_bits_in();
+    blk_op = wr.op;
     if (!rd.template bits<STRICT>(3, v)) {
       status = ZT_E_INPUT_BROKEN;
       break;
@@ -373,8 +380,17 @@ __device__ __forceinline__ void inflate_stream(const InfJob &job, InfResult &res
     rd.ip_ref = (rd.pos_bits_in() + 7) >> 3;
   }
   wave_sync();
-  if (status == ZT_OK) wr.flush(wr.op);
+  if (status == ZT_OK) {
+    wr.flush(wr.op);
+    blk_bits = rd.pos_bits_in();
+    blk_op = wr.op;
+  } else if (job.resume) {
+    wr.flush(blk_op);  // the complete blocks (ring bytes [blk_op - 32 KiB, op) are still held)
+  }
   if (lane == 0) {
+    res.blk_bits = blk_bits;
+    res.blk_op = blk_op;
+    res.stop_bits = rd.pos_bits_in();
     res.out_len = wr.op;
     res.end_ip = STRICT ? rd.ip_ref : (rd.pos_bits_in() + 7) >> 3;
     res.status = status;

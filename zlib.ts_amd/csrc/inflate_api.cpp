@@ -384,6 +384,83 @@ int zt_inflate_raw(const uint8_t *in, size_t n, size_t index, const zt_inflate_o
   return rc;
 }
 
+int zt_inflate_raw_resume(const uint8_t *in, size_t n, uint64_t bit_pos, const uint8_t *window, size_t wlen,
+                          uint8_t **out, size_t *out_len, uint64_t *end_bits, int *finished) {
+  if (!out || !out_len || !end_bits || !finished) return set_error(ZT_E_ARG, "null output");
+  if ((n && !in) || (wlen && !window)) return set_error(ZT_E_ARG, "null input");
+  if (bit_pos > (uint64_t)n * 8) return set_error(ZT_E_ARG, "bit position past the end of the input");
+  *out = nullptr;
+  *out_len = 0;
+  *end_bits = bit_pos;
+  *finished = 0;
+  if (wlen > 32768) {  // only the last 32 KiB can be referenced
+    window += wlen - 32768;
+    wlen = 32768;
+  }
+  // the decoder reads the caller's bytes from the byte holding bit_pos on
+  // (byte alignment kept: stored blocks stay aligned), skips the bits of that
+  // byte already used, and starts with the window in its history
+  const size_t byte = (size_t)(bit_pos >> 3);
+  const unsigned sh = (unsigned)(bit_pos & 7);
+  const size_t m = n - byte;
+  if ((uint64_t)m * 8 <= sh) return ZT_OK;  // nothing new to decode
+  DeviceCtx *c;
+  ZT_TRY(get_ctx(&c));
+  std::lock_guard<std::recursive_mutex> ctx_lock(c->mu);
+  void *d_in, *d_jobs;
+  const size_t in_bytes = align_up(m, 256);
+  ZT_TRY(scratch(c, 0, in_bytes + wlen + 16, &d_in));
+  ZT_TRY(upload(c, d_in, in + byte, m, c->stream));
+  const uint8_t *d_hist = (const uint8_t *)d_in + in_bytes;
+  if (wlen) ZT_HIP(hipMemcpyAsync((void *)d_hist, window, wlen, hipMemcpyHostToDevice, c->stream));
+  ZT_TRY(scratch(c, 2, sizeof(InfJob) + sizeof(InfResult) + 256, &d_jobs));
+  InfResult *d_res = (InfResult *)((uint8_t *)d_jobs + align_up(sizeof(InfJob), 256));
+  size_t cap = std::max<size_t>(65536, m * 4);
+  for (int pass = 0; pass < 2; ++pass) {
+    void *d_out;
+    ZT_TRY(scratch(c, 1, cap, &d_out));
+    InfJob j{};
+    j.in = (const uint8_t *)d_in;
+    j.n = m;
+    j.out = (uint8_t *)d_out;
+    j.cap = cap;
+    j.resume = 1;
+    j.start_bit = sh;
+    j.hist = d_hist;
+    j.hist_len = (uint32_t)wlen;
+    InfResult r;
+    ZT_HIP(hipMemcpyAsync(d_jobs, &j, sizeof j, hipMemcpyHostToDevice, c->stream));
+    ZT_TRY(inflate_jobs_dev((const InfJob *)d_jobs, d_res, 1, c->stream));
+    ZT_HIP(hipMemcpyAsync(&r, d_res, sizeof r, hipMemcpyDeviceToHost, c->stream));
+    ZT_HIP(hipStreamSynchronize(c->stream));
+    // running out of input (the reader's end-of-input statuses, or any error
+    // within the last 64 bits, where a peek may have seen the zeros past the
+    // end) means "more input needed"; an error before that is the stream's own
+    const bool truncated = r.status == ZT_E_INPUT_BROKEN || r.status == ZT_E_STORED_LEN ||
+                           r.status == ZT_E_STORED_NLEN || r.status == ZT_E_INVALID_CODE_LENGTH ||
+                           r.stop_bits + 64 > (uint64_t)m * 8;
+    if (r.status != ZT_OK && !truncated) return inflate_error(r.status, r.detail);
+    const uint64_t done = (r.status == ZT_OK ? r.out_len : r.blk_op) - wlen;  // new bytes
+    if (done > cap) {  // decoded past the output guess: again with the exact size
+      cap = (size_t)done;
+      continue;
+    }
+    uint8_t *h = (uint8_t *)malloc(done ? done : 1);
+    if (!h) return set_error(ZT_E_NOMEM, "host allocation failed");
+    const int rc = download(c, h, d_out, done, c->stream);
+    if (rc) {
+      free(h);
+      return rc;
+    }
+    *out = h;
+    *out_len = done;
+    *end_bits = (uint64_t)byte * 8 + r.blk_bits;
+    *finished = r.status == ZT_OK ? 1 : 0;
+    return ZT_OK;
+  }
+  return set_error(ZT_E_INTERNAL, "resume: output size did not settle");
+}
+
 int zt_inflate_raw_batch(const uint8_t *const *in, const size_t *n, size_t count, const zt_inflate_opts *opts,
                          uint8_t **out, size_t *out_len, size_t *end_ip, int *status) {
   if (count == 0) return ZT_OK;

@@ -158,6 +158,10 @@ struct InfJob {
   uint8_t *out;       // output buffer (device)
   uint64_t cap;       // output capacity; decoding continues past it, counting only
   int32_t strict;     // stop with 'input buffer is broken' where the reference's EOF test throws
+  int32_t resume;     // on an error, still write the output of the blocks that decoded completely
+  uint32_t start_bit;      // resume: bits of in[start] already used
+  uint32_t hist_len;       // resume: output already produced (match history), <= 32 KiB ...
+  const uint8_t *hist;     // ... its bytes (device); `out` receives only the new bytes
   uint32_t stop_first;        // segment decode: first candidate index to test
   const uint64_t *stops;      // sorted segment starts (byte positions in `in`), or null
   uint64_t stop_count;
@@ -170,6 +174,12 @@ struct InfResult {
   int32_t detail;       // code length / BTYPE for the message
   int32_t strict_fail;  // reference's readBits EOF check would throw
   int32_t stop_idx;     // segment decode: index of the segment start where decoding stopped, -1 at BFINAL
+  // resumable decode (zt_inflate_raw_resume): the bit position (relative to
+  // `in`) right after the last block that decoded completely and the output
+  // length there; the reader's bit position when decoding stopped
+  uint64_t blk_bits;
+  uint64_t blk_op;
+  uint64_t stop_bits;
 };
 
 // segment-parallel inflate (restart markers written by deflate); returns 1 when

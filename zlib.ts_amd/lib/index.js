@@ -1,6 +1,8 @@
 // zlib.ts_amd: the reference's hot-path classes over the MI355X engine.
 export { RawDeflate, CompressionType } from './RawDeflate.js';
 export { RawInflate, BufferType } from './RawInflate.js';
+export { RawInflateStream } from './RawInflateStream.js';
+export { InflateStream } from './InflateStream.js';
 export { CRC32 } from './CRC32.js';
 export { Adler32 } from './Adler32.js';
 export { GZip, GZipFlagsMask, GZipMagicNumber, GZipOperatingSystem } from './GZip.js';

@@ -170,6 +170,29 @@ void set_num(napi_env env, napi_value obj, const char *k, double v) {
   napi_set_named_property(env, obj, k, x);
 }
 
+// inflateResume(input: Uint8Array, bitPos, window: Uint8Array) -> {output, endBits, finished}
+napi_value inflate_resume(napi_env env, napi_callback_info info) {
+  napi_value a[3];
+  args(env, info, a, 3);
+  const uint8_t *p, *w;
+  size_t n, wn;
+  if (!get_u8(env, a[0], &p, &n) || !get_u8(env, a[2], &w, &wn)) return nullptr;
+  const int64_t bit = get_i64(env, a[1], 0);
+  uint8_t *out = nullptr;
+  size_t olen = 0;
+  uint64_t end = 0;
+  int fin = 0;
+  int rc = zt_inflate_raw_resume(p, n, bit < 0 ? 0 : (uint64_t)bit, w, wn, &out, &olen, &end, &fin);
+  if (rc) return throw_zt(env, rc);
+  napi_value obj, f;
+  napi_create_object(env, &obj);
+  napi_set_named_property(env, obj, "output", new_u8(env, out, olen));
+  set_num(env, obj, "endBits", (double)end);
+  napi_get_boolean(env, fin != 0, &f);
+  napi_set_named_property(env, obj, "finished", f);
+  return obj;
+}
+
 // optional Uint8Array argument (undefined / null -> absent)
 bool opt_u8(napi_env env, napi_value v, const uint8_t **p, size_t *n, bool *present) {
   napi_valuetype t;
@@ -421,6 +444,7 @@ napi_value init(napi_env env, napi_value exports) {
       {"adler32Update", nullptr, adler32_update, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"deflateRaw", nullptr, deflate_raw, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"inflateRaw", nullptr, inflate_raw, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+      {"inflateResume", nullptr, inflate_resume, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"gzipCompress", nullptr, gzip_compress, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"gunzip", nullptr, gunzip, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"zlibCompress", nullptr, zlib_compress, nullptr, nullptr, nullptr, napi_enumerable, nullptr},

@@ -18,7 +18,7 @@ ERRORS = {
     -30: "ZT_E_GZIP_SIGNATURE", -31: "ZT_E_GZIP_METHOD", -32: "ZT_E_GZIP_HCRC", -33: "ZT_E_GZIP_CRC32",
     -34: "ZT_E_GZIP_ISIZE", -40: "ZT_E_ZLIB_METHOD", -41: "ZT_E_ZLIB_FCHECK", -42: "ZT_E_ZLIB_FDICT",
     -43: "ZT_E_ZLIB_ADLER", -100: "ZT_E_NO_DEVICE",
-    -101: "ZT_E_HIP", -102: "ZT_E_NOMEM", -103: "ZT_E_ARG",
+    -101: "ZT_E_HIP", -102: "ZT_E_NOMEM", -103: "ZT_E_ARG", -104: "ZT_E_INTERNAL",
 }
 
 
@@ -101,6 +101,8 @@ def _load():
         "zt_checksums": ([vp, sz, u32, u32, P(u32), P(u32)], ctypes.c_int),
         "zt_deflate_raw": ([vp, sz, P(DeflateOpts), u8pp, P(sz)], ctypes.c_int),
         "zt_inflate_raw": ([vp, sz, sz, P(InflateOpts), u8pp, P(sz), P(sz)], ctypes.c_int),
+        "zt_inflate_raw_resume": ([vp, sz, ctypes.c_uint64, vp, sz, u8pp, P(sz), P(ctypes.c_uint64),
+                                   P(ctypes.c_int)], ctypes.c_int),
         "zt_inflate_raw_batch": ([P(vp), P(sz), sz, P(InflateOpts), u8pp, P(sz), P(sz), P(ctypes.c_int)],
                                  ctypes.c_int),
         "zt_deflate_raw_batch": ([P(vp), P(sz), sz, P(DeflateOpts), u8pp, P(sz), P(ctypes.c_int)], ctypes.c_int),
@@ -140,7 +142,7 @@ lib = _load()
 # every symbol include/zt.h declares (checked by tests/test_abi.py)
 SYMBOLS = [
     "zt_device_count", "zt_set_device", "zt_set_devices", "zt_last_error_message", "zt_version", "zt_free", "zt_crc32_update",
-    "zt_adler32_update", "zt_checksums", "zt_deflate_raw", "zt_inflate_raw", "zt_inflate_raw_batch",
+    "zt_adler32_update", "zt_checksums", "zt_deflate_raw", "zt_inflate_raw", "zt_inflate_raw_resume", "zt_inflate_raw_batch",
     "zt_deflate_raw_batch", "zt_gzip_compress", "zt_gzip_compress_batch", "zt_zlib_compress_batch", "zt_gunzip",
     "zt_crc32_batch", "zt_zip_compress", "zt_unzip", "zt_zlib_compress", "zt_zlib_decompress",
     "zt_dev_checksums", "zt_deflate_plan_create", "zt_deflate_plan_destroy",
@@ -216,6 +218,52 @@ def inflate_raw(data, index=0, ref_strict=False, buffer_type=1, buffer_size=0x80
     res = ctypes.string_at(out, olen.value)
     lib.zt_free(out)
     return res, ip.value
+
+
+def inflate_raw_resume(data, bit_pos=0, window=b""):
+    """zt_inflate_raw_resume: (output of the complete blocks, end bit, finished)."""
+    b, n = _cbuf(data)
+    w, wn = _cbuf(window)
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    olen = ctypes.c_size_t()
+    end = ctypes.c_uint64()
+    fin = ctypes.c_int()
+    _check(lib.zt_inflate_raw_resume(b, n, bit_pos, w, wn, ctypes.byref(out), ctypes.byref(olen), ctypes.byref(end),
+                                     ctypes.byref(fin)))
+    res = ctypes.string_at(out, olen.value) if out else b""
+    if out:
+        lib.zt_free(out)
+    return res, end.value, bool(fin.value)
+
+
+class RawInflateStream:
+    """The reference's streaming decoder surface (src/RawInflateStream.ts:
+    52-120): ``decompress(new_input, ip)`` decodes what the input holds so far
+    and returns the bytes produced by this call.  State between calls: the
+    input position (byte ``ip`` and the bits of it already used), the last 32
+    KiB of output (match history) and whether the final block was seen."""
+
+    def __init__(self, data=b"", ip=0):
+        self.input = bytes(data)
+        self.ip = ip
+        self.bit = 0
+        self.window = b""
+        self.bfinal = False
+        self.total = 0
+
+    def decompress(self, new_input=None, ip=None):
+        if new_input is not None:
+            self.input = bytes(new_input)
+        if ip is not None:  # (a re-based buffer: the bits of its byte `ip` already used stay used)
+            self.ip = ip
+        if self.bfinal or self.ip >= len(self.input):
+            return b""
+        out, end, fin = inflate_raw_resume(self.input, self.ip * 8 + self.bit, self.window)
+        self.ip, self.bit = end >> 3, end & 7
+        self.bfinal = fin
+        self.total += len(out)
+        self.window = (self.window + out)[-32768:]
+        return out
 
 
 def inflate_raw_batch(streams, ref_strict=False):
