@@ -33,8 +33,11 @@ namespace {
 #ifndef ZT_CK_THREADS
 #define ZT_CK_THREADS 256
 #endif
+#ifndef ZT_CK_Q
+#define ZT_CK_Q 2  // 16-byte loads per lane per row: a lane's piece of a row is 16 Q contiguous bytes
+#endif
 #ifndef ZT_CK_B
-#define ZT_CK_B 8
+#define ZT_CK_B (8 / ZT_CK_Q)  // rows per batch (8 loads per lane in flight)
 #endif
 constexpr int CK_THREADS = ZT_CK_THREADS;            // 4 waves per workgroup, 3 workgroups per CU (LDS)
 constexpr int CK_SLICE = 262144 / CK_THREADS;        // bytes per thread (ragged segments)
@@ -42,6 +45,10 @@ constexpr size_t CK_SEG = (size_t)CK_THREADS * CK_SLICE;  // 256 KiB per segment
 constexpr int NIB_ENTRIES = ZT_CRC_NIB_N;            // (16 + 8) nibble positions x 16 values
 constexpr int ADV = 16;                              // first nibble table of x^(8*1024) * v
 constexpr int CK_WAVE_BYTES = 262144 / (CK_THREADS / 64);  // contiguous bytes per wave in a whole segment
+constexpr int CK_Q = ZT_CK_Q;
+constexpr int CK_P = 16 * CK_Q;   // a lane's contiguous bytes per row
+constexpr int CK_RB = 64 * CK_P;  // bytes per row (one wave: 64 lanes x CK_P)
+static_assert(CK_WAVE_BYTES % (CK_RB * ZT_CK_B) == 0, "rows tile the wave's bytes");
 static_assert(CK_WAVE_BYTES * (CK_THREADS / 64) == (int)CK_SEG, "waves tile the segment");
 
 // batch checksums: segment k of the buffer at frame + off (off 16-byte aligned)
@@ -80,12 +87,7 @@ __device__ __forceinline__ uint32_t crc_step8(uint32_t c, uint32_t w0, uint32_t 
   return r;
 }
 
-// raw CRC (state 0) of the 16 bytes v
-__device__ __forceinline__ uint32_t crc_raw16(uint4 v, const uint32_t *T, int lane) {
-  return crc_step8(crc_step8(0u, v.x, v.y, T, lane), v.z, v.w, T, lane);
-}
-
-// c * x^(8 * 1024) mod P (the lane stream's advance by one 1 KiB row)
+// c * x^(8 * CK_RB) mod P (the lane stream's advance by one row)
 __device__ __forceinline__ uint32_t crc_adv1k(uint32_t c, const uint32_t *T, int lane) {
   uint32_t r = 0;
 #pragma unroll
@@ -176,46 +178,68 @@ __global__ __launch_bounds__(CK_THREADS) void checksum_segments(const uint8_t *_
     const bool whole = seg_lo >= lo && seg_lo + CK_SEG <= hi;
     uint64_t a1 = 0, a2 = 0;  // Adler sums of this thread's bytes, positions weighted to the segment end
     if (whole) {
-      // coalesced lane stream: wave w's 64 KiB, lane l's pieces at 1024 k + 16 l
+      // coalesced lane stream: wave w's 64 KiB in rows of CK_RB bytes, lane
+      // l's piece of row k the CK_P bytes at CK_RB k + CK_P l (CK_Q loads of
+      // 16 bytes); the lane's CRC advances once per row, so its lookups per
+      // byte are 2 + 0.5 / CK_Q
       const int wv = tid >> 6, ln = tid & 63;
-      const uint4 *p = reinterpret_cast<const uint4 *>(frame + seg_lo + (size_t)wv * CK_WAVE_BYTES) + ln;
-      uint32_t L = 0, S = 0, KS = 0, W = 0;
-      constexpr int ROWS = CK_WAVE_BYTES / 1024, B = ZT_CK_B;
-      uint4 v[B], nx[B];
+      const uint4 *p = reinterpret_cast<const uint4 *>(frame + seg_lo + (size_t)wv * CK_WAVE_BYTES) + ln * CK_Q;
+      uint32_t L = 0, S = 0, KS = 0, JS = 0, W = 0;
+      constexpr int ROWS = CK_WAVE_BYTES / CK_RB, B = ZT_CK_B;
+      constexpr int RQ = CK_RB / 16;  // uint4 per row
+      uint4 v[B * CK_Q], nx[B * CK_Q];
 #pragma unroll
-      for (int k = 0; k < B; ++k) v[k] = ld_stream(p + k * 64);
+      for (int k = 0; k < B; ++k)
+#pragma unroll
+        for (int j = 0; j < CK_Q; ++j) v[k * CK_Q + j] = ld_stream(p + k * RQ + j);
 #pragma unroll 1
       for (int r0 = 0; r0 < ROWS; r0 += B) {
         if (r0 + B < ROWS) {
 #pragma unroll
-          for (int k = 0; k < B; ++k) nx[k] = ld_stream(p + (r0 + B + k) * 64);
+          for (int k = 0; k < B; ++k)
+#pragma unroll
+            for (int j = 0; j < CK_Q; ++j) nx[k * CK_Q + j] = ld_stream(p + (r0 + B + k) * RQ + j);
         }
 #pragma unroll
         for (int k = 0; k < B; ++k) {
-          if (DO_CRC) L = crc_adv1k(L, T, lane32) ^ crc_raw16(v[k], T, lane32);
+          if (DO_CRC) {
+            uint32_t r = 0;  // raw CRC of the lane's piece
+#pragma unroll
+            for (int j = 0; j < CK_Q; ++j) {
+              const uint4 x = v[k * CK_Q + j];
+              r = crc_step8(crc_step8(r, x.x, x.y, T, lane32), x.z, x.w, T, lane32);
+            }
+            L = crc_adv1k(L, T, lane32) ^ r;
+          }
           if (DO_ADLER) {
-            uint32_t wsum = __builtin_amdgcn_udot4(v[k].x, 0x0D0E0F10u, 0u, false);
-            wsum = __builtin_amdgcn_udot4(v[k].y, 0x090A0B0Cu, wsum, false);
-            wsum = __builtin_amdgcn_udot4(v[k].z, 0x05060708u, wsum, false);
-            wsum = __builtin_amdgcn_udot4(v[k].w, 0x01020304u, wsum, false);
-            uint32_t sk = __builtin_amdgcn_udot4(v[k].x, 0x01010101u, 0u, false);
-            sk = __builtin_amdgcn_udot4(v[k].y, 0x01010101u, sk, false);
-            sk = __builtin_amdgcn_udot4(v[k].z, 0x01010101u, sk, false);
-            sk = __builtin_amdgcn_udot4(v[k].w, 0x01010101u, sk, false);
-            S += sk;
-            KS += (uint32_t)(r0 + k) * sk;
-            W += wsum;
+#pragma unroll
+            for (int j = 0; j < CK_Q; ++j) {
+              const uint4 x = v[k * CK_Q + j];
+              uint32_t wsum = __builtin_amdgcn_udot4(x.x, 0x0D0E0F10u, 0u, false);
+              wsum = __builtin_amdgcn_udot4(x.y, 0x090A0B0Cu, wsum, false);
+              wsum = __builtin_amdgcn_udot4(x.z, 0x05060708u, wsum, false);
+              wsum = __builtin_amdgcn_udot4(x.w, 0x01020304u, wsum, false);
+              uint32_t sk = __builtin_amdgcn_udot4(x.x, 0x01010101u, 0u, false);
+              sk = __builtin_amdgcn_udot4(x.y, 0x01010101u, sk, false);
+              sk = __builtin_amdgcn_udot4(x.z, 0x01010101u, sk, false);
+              sk = __builtin_amdgcn_udot4(x.w, 0x01010101u, sk, false);
+              S += sk;
+              KS += (uint32_t)(r0 + k) * sk;
+              JS += (uint32_t)j * sk;
+              W += wsum;
+            }
           }
         }
 #pragma unroll
-        for (int k = 0; k < B; ++k) v[k] = nx[k];
+        for (int k = 0; k < B * CK_Q; ++k) v[k] = nx[k];
       }
       c = L;
       len = CK_SLICE;
-      // byte j of row k sits CK_SEG - (64 KiB w + 1024 k + 16 l + j) bytes before the segment end
-      const uint64_t cw = (uint64_t)CK_SEG - (uint64_t)wv * CK_WAVE_BYTES - 16u * (uint32_t)ln - 16u;
+      // byte b of load j of row k sits CK_SEG - (64 KiB w + CK_RB k + CK_P l + 16 j + b)
+      // bytes before the segment end
+      const uint64_t cw = (uint64_t)CK_SEG - (uint64_t)wv * CK_WAVE_BYTES - (uint64_t)CK_P * (uint32_t)ln - 16u;
       a1 = S;
-      a2 = cw * S - 1024ull * KS + W;
+      a2 = cw * S - (uint64_t)CK_RB * KS - 16ull * JS + W;
     } else if (v_lo == s_lo && v_hi == s_lo + CK_SLICE) {
       len = CK_SLICE;
       const uint4 *p = reinterpret_cast<const uint4 *>(frame + s_lo);
@@ -434,18 +458,18 @@ void crc_host_tables(uint32_t byte_table[256], uint32_t nib[ZT_CRC_NIB_N], uint3
   }
   x2n[0] = 1u << 30;  // x^1
   for (int k = 1; k < 32; ++k) x2n[k] = multmodp(x2n[k - 1], x2n[k - 1]);
-  // nib[(ADV + j) * 16 + v]: (v << 4 j) * x^(8 * 1024) mod P
-  const uint32_t k1 = x2nmodp(x2n, 1024, 3);
+  // nib[(ADV + j) * 16 + v]: (v << 4 j) * x^(8 * CK_RB) mod P
+  const uint32_t k1 = x2nmodp(x2n, CK_RB, 3);
   for (int j = 0; j < 8; ++j)
     for (uint32_t v = 0; v < 16; ++v) nib[(ADV + j) * 16 + v] = multmodp(k1, v << (4 * j));
 }
 
 void crc_shift_tables(const uint32_t x2n[32], uint32_t shift[ZT_CRC_SHIFT_N]) {
-  // lane streams of a whole segment: thread t = 64 w + l ends 16 bytes past
-  // W w + W - 1 KiB + 16 l (W = CK_WAVE_BYTES), i.e. W (waves - 1 - w) + 1008 - 16 l
-  // before the segment end
+  // lane streams of a whole segment: thread t = 64 w + l ends CK_P bytes past
+  // W w + W - CK_RB + CK_P l (W = CK_WAVE_BYTES), i.e. W (waves - 1 - w) +
+  // CK_RB - CK_P (l + 1) before the segment end
   for (int t = 0; t < CK_THREADS; ++t) {
-    const uint64_t after = (uint64_t)CK_WAVE_BYTES * (CK_THREADS / 64 - 1 - t / 64) + 1024 - 16 - 16 * (t % 64);
+    const uint64_t after = (uint64_t)CK_WAVE_BYTES * (CK_THREADS / 64 - 1 - t / 64) + CK_RB - CK_P * (t % 64 + 1);
     shift[ZT_CRC_LANE_OFF + t] = x2nmodp(x2n, after, 3);
   }
   // digit tables: x^(8 * v * 64^d)

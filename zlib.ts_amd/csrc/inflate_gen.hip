@@ -580,7 +580,7 @@ struct CopyShared16 {
 __device__ __forceinline__ uint32_t cp_val16(const CopyShared16 *sh, uint64_t op, uint32_t d, int32_t &off) {
   const uint32_t rv = sh->ring[((uint32_t)op - d - 1) & RING_MASK];
   const bool lit = (d & 0x8000u) != 0;
-  off = (lit && (d & 0x100u)) ? (int32_t)(d & 0xFF) : -1;
+  off = (lit && (d & 0x4000u)) ? (int32_t)(d & 0x3FF) : -1;
   return lit ? (d & 0xFF) : rv;
 }
 
@@ -611,7 +611,7 @@ __global__ __launch_bounds__(64) void copy_marker_kernel(ResolveParams P, const 
   const uint64_t nchunks = (n + 127) / 128;
   uint64_t issued = 0, flushed = 0;
   for (uint64_t op = 0; op < n; op += CP_STEP) {
-    const uint64_t need = (op >> 7) + 2 < nchunks ? (op >> 7) + 2 : nchunks;
+    const uint64_t need = (op >> 7) + CP_STEP / 128 < nchunks ? (op >> 7) + CP_STEP / 128 : nchunks;
     const uint64_t want = need + CP_AHEAD < nchunks ? need + CP_AHEAD : nchunks;
     while (issued < want) {
       __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint32_t *>(dsrc + issued * 128) + lane,
@@ -622,16 +622,28 @@ __global__ __launch_bounds__(64) void copy_marker_kernel(ResolveParams P, const 
       __builtin_amdgcn_s_waitcnt(cp_vmcnt(CP_AHEAD));
     else
       __builtin_amdgcn_s_waitcnt(0x0F70);
-    const uint32_t x = (uint32_t)op + 4 * (uint32_t)lane;
-    const uint64_t dd = *reinterpret_cast<const uint64_t *>(&sh.desc[x & (CP_DESC_RING - 1)]);
-    int32_t o0, o1, o2, o3;
-    const uint32_t b0 = cp_val16(&sh, op, (uint32_t)dd & 0xFFFF, o0);
-    const uint32_t b1 = cp_val16(&sh, op, (uint32_t)(dd >> 16) & 0xFFFF, o1);
-    const uint32_t b2 = cp_val16(&sh, op, (uint32_t)(dd >> 32) & 0xFFFF, o2);
-    const uint32_t b3 = cp_val16(&sh, op, (uint32_t)(dd >> 48), o3);
-    if (__ballot(o0 >= 0 || o1 >= 0 || o2 >= 0 || o3 >= 0) == 0) {
-      *reinterpret_cast<uint64_t *>(&sh.ring[x & RING_MASK]) =
-          (uint64_t)b0 | ((uint64_t)b1 << 16) | ((uint64_t)b2 << 32) | ((uint64_t)b3 << 48);
+    uint64_t dd[CP_G];
+#pragma unroll
+    for (int g = 0; g < CP_G; ++g) {
+      const uint32_t x = (uint32_t)op + 256u * g + 4 * (uint32_t)lane;
+      dd[g] = *reinterpret_cast<const uint64_t *>(&sh.desc[x & (CP_DESC_RING - 1)]);
+    }
+    uint64_t bw[CP_G];
+    bool in_step = false;
+#pragma unroll
+    for (int g = 0; g < CP_G; ++g) {
+      int32_t o0, o1, o2, o3;
+      const uint32_t b0 = cp_val16(&sh, op, (uint32_t)dd[g] & 0xFFFF, o0);
+      const uint32_t b1 = cp_val16(&sh, op, (uint32_t)(dd[g] >> 16) & 0xFFFF, o1);
+      const uint32_t b2 = cp_val16(&sh, op, (uint32_t)(dd[g] >> 32) & 0xFFFF, o2);
+      const uint32_t b3 = cp_val16(&sh, op, (uint32_t)(dd[g] >> 48), o3);
+      bw[g] = (uint64_t)b0 | ((uint64_t)b1 << 16) | ((uint64_t)b2 << 32) | ((uint64_t)b3 << 48);
+      in_step = in_step || o0 >= 0 || o1 >= 0 || o2 >= 0 || o3 >= 0;
+    }
+    if (__ballot(in_step) == 0) {
+#pragma unroll
+      for (int g = 0; g < CP_G; ++g)
+        *reinterpret_cast<uint64_t *>(&sh.ring[((uint32_t)op + 256u * g + 4 * (uint32_t)lane) & RING_MASK]) = bw[g];
     } else {
       for (uint32_t sub = 0; sub < CP_STEP; sub += 64) {
         const uint64_t y = op + sub + (uint64_t)lane;

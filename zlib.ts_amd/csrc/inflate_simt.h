@@ -487,16 +487,21 @@ __device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t src_lane) {
 constexpr uint32_t RS_TOK_RING = 1024;        // tokens staged in LDS (16 chunks of 64)
 constexpr uint32_t RS_AHEAD = 12;             // chunks in flight ahead of the cursor
 constexpr uint32_t RS_FLUSH = 8192;           // output flush granule
-constexpr uint32_t CP_STEP = 256;  // copy_kernel bytes per step
+#ifndef ZT_CP_STEP
+#define ZT_CP_STEP 512
+#endif
+constexpr uint32_t CP_STEP = ZT_CP_STEP;  // copy_kernel bytes per step (a multiple of 256)
+constexpr int CP_G = CP_STEP / 256;       // 4-byte groups per lane per step
 #ifndef ZT_CP_RING
-#define ZT_CP_RING 2048
+#define ZT_CP_RING (CP_STEP <= 256 ? 2048 : 4096)
 #endif
 #ifndef ZT_CP_AHEAD
-#define ZT_CP_AHEAD 12
+#define ZT_CP_AHEAD (CP_STEP <= 256 ? 12 : 24)
 #endif
 constexpr uint32_t CP_DESC_RING = ZT_CP_RING;  // descriptors staged in LDS (chunks of 128)
 constexpr uint32_t CP_AHEAD = ZT_CP_AHEAD;      // chunks in flight ahead of the step
-static_assert((CP_AHEAD + 2) * 128 <= CP_DESC_RING && CP_AHEAD < 64, "descriptor ring");
+static_assert(CP_STEP % 256 == 0 && (CP_STEP & (CP_STEP - 1)) == 0, "copy step");
+static_assert((CP_AHEAD + CP_STEP / 128) * 128 <= CP_DESC_RING && CP_AHEAD < 64, "descriptor ring");
 // s_waitcnt vmcnt(v) with lgkmcnt / expcnt left alone (vmcnt bits 3:0 and 15:14)
 constexpr int cp_vmcnt(uint32_t v) { return (int)(0x0F70u | (v & 15u) | ((v >> 4) << 14)); }
 

@@ -203,7 +203,7 @@ __device__ __forceinline__ uint32_t tok_len(uint32_t t) { return (t >> 16) ? (t 
 // 255 back), so such a copy becomes an in-step reference to the byte it came
 // from, which copy_kernel resolves from the step itself.
 __device__ __forceinline__ uint32_t safe_desc(uint32_t d, uint32_t step_off) {
-  return ((d & 0x8000u) || d < 32768u - CP_STEP) ? d : (0x8100u | step_off);
+  return ((d & 0x8000u) || d < 32768u - CP_STEP) ? d : (0xC000u | step_off);
 }
 
 struct ExpandShared {
@@ -260,7 +260,7 @@ __global__ __launch_bounds__(64) void expand_kernel(ResolveParams P) {
     const uint32_t owner = __popcll(starts & (~0ull >> (63 - lane)));  // token of byte `lane`
     const uint32_t tj = bperm(t, owner);
     const uint32_t ej = bperm(S - len, owner);  // the token's start, relative to the cursor token
-    // descriptor: 0x8000 | byte (literal), 0x8100 | o (= byte ws + o, before
+    // descriptor: 0x8000 | byte (literal), 0xC000 | o (= byte ws + o, before
     // this unit), or ws - src - 1 (a byte before the copy step); references
     // into the step are followed here (earlier windows from LDS, this window
     // by pointer jumping over the lanes)
@@ -284,7 +284,7 @@ __global__ __launch_bounds__(64) void expand_kernel(ResolveParams P) {
           if (src < (int64_t)ws)
             dsc = (uint32_t)((int64_t)ws - src - 1);
           else if (src < (int64_t)back)
-            dsc = 0x8100u | (uint32_t)(src - (int64_t)ws);  // before this unit: copy_kernel resolves it
+            dsc = 0xC000u | (uint32_t)(src - (int64_t)ws);  // before this unit: copy_kernel resolves it
           else if (src < (int64_t)pos)
             dsc = safe_desc(sh.cw[src - (int64_t)ws], (uint32_t)(src - (int64_t)ws));  // an earlier window
           else
@@ -349,7 +349,7 @@ __device__ __forceinline__ void cp_flush(const CopyShared *sh, uint8_t *out, uin
 __device__ __forceinline__ uint32_t cp_byte(const CopyShared *sh, uint64_t op, uint32_t d, int32_t &off) {
   const uint32_t rv = sh->ring[((uint32_t)op - d - 1) & RING_MASK];
   const bool lit = (d & 0x8000u) != 0;
-  off = (lit && (d & 0x100u)) ? (int32_t)(d & 0xFF) : -1;
+  off = (lit && (d & 0x4000u)) ? (int32_t)(d & 0x3FF) : -1;  // 0xC000 | o: the byte op + o of this step
   return lit ? (d & 0xFF) : rv;
 }
 
@@ -368,7 +368,7 @@ __global__ __launch_bounds__(64) void copy_kernel(ResolveParams P) {
   uint64_t issued = 0;
   uint64_t flushed = 0;
   for (uint64_t op = 0; op < n; op += CP_STEP) {
-    const uint64_t need = (op >> 7) + 2 < nchunks ? (op >> 7) + 2 : nchunks;
+    const uint64_t need = (op >> 7) + CP_STEP / 128 < nchunks ? (op >> 7) + CP_STEP / 128 : nchunks;
     const uint64_t want = need + CP_AHEAD < nchunks ? need + CP_AHEAD : nchunks;
     while (issued < want) {
       __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint32_t *>(dsrc + issued * 128) + lane,
@@ -379,16 +379,32 @@ __global__ __launch_bounds__(64) void copy_kernel(ResolveParams P) {
       __builtin_amdgcn_s_waitcnt(cp_vmcnt(CP_AHEAD));
     else
       __builtin_amdgcn_s_waitcnt(0x0F70);
-    // lane j: bytes op + 4 j .. op + 4 j + 3 (bytes past n are never flushed)
-    const uint32_t x = (uint32_t)op + 4 * (uint32_t)lane;  // ring / descriptor index (masked)
-    const uint64_t dd = *reinterpret_cast<const uint64_t *>(&sh.desc[x & (CP_DESC_RING - 1)]);
-    int32_t o0, o1, o2, o3;
-    const uint32_t b0 = cp_byte(&sh, op, (uint32_t)dd & 0xFFFF, o0);
-    const uint32_t b1 = cp_byte(&sh, op, (uint32_t)(dd >> 16) & 0xFFFF, o1);
-    const uint32_t b2 = cp_byte(&sh, op, (uint32_t)(dd >> 32) & 0xFFFF, o2);
-    const uint32_t b3 = cp_byte(&sh, op, (uint32_t)(dd >> 48), o3);
-    if (__ballot(o0 >= 0 || o1 >= 0 || o2 >= 0 || o3 >= 0) == 0) {
-      *reinterpret_cast<uint32_t *>(&sh.ring[x & RING_MASK]) = b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+    // lane j: bytes op + 256 g + 4 j .. + 3 for each group g (bytes past n
+    // are never flushed); every byte of a step is a literal or a ring byte
+    // before the step, so all descriptor reads, then all ring reads, are
+    // issued before any write
+    uint64_t dd[CP_G];
+#pragma unroll
+    for (int g = 0; g < CP_G; ++g) {
+      const uint32_t x = (uint32_t)op + 256u * g + 4 * (uint32_t)lane;  // ring / descriptor index (masked)
+      dd[g] = *reinterpret_cast<const uint64_t *>(&sh.desc[x & (CP_DESC_RING - 1)]);
+    }
+    uint32_t bw[CP_G];
+    bool in_step = false;
+#pragma unroll
+    for (int g = 0; g < CP_G; ++g) {
+      int32_t o0, o1, o2, o3;
+      const uint32_t b0 = cp_byte(&sh, op, (uint32_t)dd[g] & 0xFFFF, o0);
+      const uint32_t b1 = cp_byte(&sh, op, (uint32_t)(dd[g] >> 16) & 0xFFFF, o1);
+      const uint32_t b2 = cp_byte(&sh, op, (uint32_t)(dd[g] >> 32) & 0xFFFF, o2);
+      const uint32_t b3 = cp_byte(&sh, op, (uint32_t)(dd[g] >> 48), o3);
+      bw[g] = b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+      in_step = in_step || o0 >= 0 || o1 >= 0 || o2 >= 0 || o3 >= 0;
+    }
+    if (__ballot(in_step) == 0) {
+#pragma unroll
+      for (int g = 0; g < CP_G; ++g)
+        *reinterpret_cast<uint32_t *>(&sh.ring[((uint32_t)op + 256u * g + 4 * (uint32_t)lane) & RING_MASK]) = bw[g];
     } else {
       // a unit boundary inside this step left references into it: resolve
       // them byte by byte (64-byte sub-steps, pointer jumping)
