@@ -74,6 +74,7 @@ constexpr int DF_SLOT = DF_BLOCK + DF_BLOCK / 8 + 1024;  // per-block slot: fits
 #endif
 constexpr uint32_t DF_HSIZE = ZT_DF_HSIZE;
 constexpr uint32_t DF_H4SIZE = ZT_DF_H4SIZE;
+static_assert(DF_HSIZE <= 65536 && DF_H4SIZE <= 65536, "bucket indices are parked in u16 slots (hash_keys)");
 constexpr int DF_THREADS = 1024;
 // the ring holds [p1 - DF_RING, p1) while sub-chunk [p0, p1) is searched;
 // a super-chunk loads DF_HIST bytes of history first (whole sub-chunks)
@@ -234,17 +235,35 @@ __device__ void load_sub(MatchShared *s, const uint8_t *g, uint32_t rel0, uint32
 // progress is published for the searching waves (match_kernel).  T = 0: the
 // 8-byte-key chains (head -> prev, s->linked); T = 1, by a second wave at the
 // same time: the 4-byte-key table (head4 -> link4, s->linked4).
-constexpr int CL_U = 8;  // steps per group: hashes, then exchanges, then links
+// Hashes of the keys at positions [lo, hi), by all threads of the workgroup,
+// parked in the slots their links will fill: prev[ridx(p)] (the ring slot of
+// p held a position 32 KiB back, out of every walk's reach) and
+// link4[p % DF_SUB] (the previous sub-chunk's, whose searches are done).  The
+// serial link waves then only read them (chain_link).
+__device__ __forceinline__ void hash_keys(MatchShared *s, uint32_t lo, uint32_t hi, Key key) {
+  for (uint32_t p = lo + threadIdx.x; p < hi; p += DF_THREADS) {
+    s->prev[ridx(p)] = (uint16_t)key_hash(s, p, key);
+    s->link4[p & (DF_SUB - 1)] = (uint16_t)key4_hash(s, p);
+  }
+}
+
+#ifndef ZT_CL_U
+#define ZT_CL_U 8
+#endif
+constexpr int CL_U = ZT_CL_U;  // steps per group: hashes, then exchanges, then links
 template <int T>
 __device__ void chain_link(MatchShared *s, uint32_t lo, uint32_t hi, Key key) {
   const int lane = threadIdx.x & 63;
   const uint32_t nsteps = (hi - lo + 63) / 64;
   uint32_t hq[CL_U];
+  // the keys' hashes were computed by every thread beforehand (hash_keys)
+  // and parked in the slots the links are about to fill
   auto hashes = [&](uint32_t sb, uint32_t (&h)[CL_U]) {
 #pragma unroll
     for (int j = 0; j < CL_U; ++j) {
       const uint32_t p = lo + (sb + j) * 64 + lane;
-      h[j] = T == 0 ? key_hash(s, p < hi ? p : lo, key) : key4_hash(s, p < hi ? p : lo);
+      const uint32_t pc = p < hi ? p : lo;  // (lanes past hi: any bucket, they exchange with a dummy)
+      h[j] = T == 0 ? (uint32_t)s->prev[ridx(pc)] : (uint32_t)s->link4[pc & (DF_SUB - 1)];
     }
   };
   hashes(0, hq);
@@ -586,14 +605,22 @@ __global__ __launch_bounds__(DF_THREADS) void match_kernel(DeflateParams P) {
     const bool fast = g_aligned && n0 + DF_SUB <= re;
     uint32_t nv = 0;
     if (fast) nv = reinterpret_cast<const uint32_t *>(g + n0)[t];
+    if (link) hash_keys(&s, inserted, ih, key);
     lds_barrier();
     DF_T(t1);
     // wave 0 links the 8-byte-key chains and wave 1 the 4-byte-key table,
     // step by step; every wave (waves 0 and 1 once done) takes super-steps of
     // 256 positions in order and searches them as soon as their links are
     // final (positions only read links of older ones)
+#ifdef ZT_DF_LINK_PRIO
+    // the linking waves are on every searcher's critical path: issue first
+    if (t < 128 && link) __builtin_amdgcn_s_setprio(ZT_DF_LINK_PRIO);
+#endif
     if (t < 64 && link) chain_link<0>(&s, inserted, ih, key);
     if (t >= 64 && t < 128 && link) chain_link<1>(&s, inserted, ih, key);
+#ifdef ZT_DF_LINK_PRIO
+    if (t < 128 && link) __builtin_amdgcn_s_setprio(0);
+#endif
 #ifdef ZT_DF_TIME
     uint64_t tl;
     DF_T(tl);
