@@ -230,3 +230,20 @@ def test_two_phase_inflate_is_used(zt, oracle):
         s = zt.deflate_raw(d, level=lvl)
         out, ip = zt.inflate_raw(s)
         assert out == d and ip == len(s)
+
+
+@pytest.mark.parametrize("level", [1, 6, 9])
+def test_output_does_not_depend_on_the_run(zt, oracle, level):
+    """The same input deflates to the same bytes whatever ran on the GPU
+    before: the match kernel must not read LDS that no thread of its own
+    workgroup wrote (a round-2 bug: the 4-byte table of the first sub-chunk's
+    last positions was read uninitialised, so level-1 streams of text
+    differed from box to box)."""
+    data = oracle.gen("wordsalad", 31, 3 << 20) + oracle.gen("structured", 31, 1 << 20)
+    first = zt.deflate_raw(data, level=level)
+    for seed in (1, 2):
+        # other work leaves other LDS contents behind on every CU
+        zt.deflate_raw(oracle.gen("xorshift32", seed, 4 << 20), level=9)
+        zt.deflate_raw(oracle.gen("wordsalad", 100 + seed, 4 << 20), level=1)
+        assert zt.deflate_raw(data, level=level) == first
+    check_stream(oracle, zt, data, first)

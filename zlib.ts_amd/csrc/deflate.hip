@@ -583,6 +583,10 @@ __global__ __launch_bounds__(DF_THREADS) void match_kernel(DeflateParams P) {
 
   for (uint32_t i = t; i < DF_HSIZE; i += DF_THREADS) s.head[i] = kNoHead;
   for (uint32_t i = t; i < DF_H4SIZE; i += DF_THREADS) s.head4[i] = kNoHead;
+  // the last kext positions of the first sub-chunk read link4 before any
+  // link reached their slots: no candidate (not the LDS left by an earlier
+  // workgroup, which made the output depend on the run)
+  for (uint32_t i = t; i < DF_SUB; i += DF_THREADS) s.link4[i] = 0;
   __syncthreads();
   uint32_t inserted = 0;  // positions [0, inserted) are in the chains
   if (re > 0) load_sub(&s, g, 0, re < DF_SUB ? re : DF_SUB);
