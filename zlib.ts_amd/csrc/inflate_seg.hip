@@ -10,6 +10,8 @@
 //      the full restart marker precedes them;
 //   2. tokenize_kernel: one wave per unit (stream start, or a sync point)
 //      decodes blocks to tokens until it reaches another sync point;
+//      (the candidate list is sorted and deduplicated, and the units' jobs
+//      written, on the device: hipcub radix sort + scan);
 //   3. the host follows the chain from the stream start (unit -> the sync
 //      point it stopped on -> the unit starting there ...), so sync points
 //      that lie inside data are never used, and cuts the chain into segments
@@ -27,6 +29,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <vector>
+
+#include <hipcub/hipcub.hpp>
 
 #include "zt_internal.h"
 
@@ -127,18 +131,38 @@ __global__ __launch_bounds__(256) void find_syncs(const uint8_t *__restrict__ in
 
 size_t align256(size_t v) { return (v + 255) & ~size_t(255); }
 
-// LSD radix sort (11-bit digits) of the sync-point list, up to `max_key`:
-// the atomic-append order of find_syncs is only roughly ascending, and a
-// comparison sort of ~32 K entries per GiB costs about 1 ms of host time
-void radix_sort(std::vector<uint64_t> &v, uint64_t max_key) {
-  std::vector<uint64_t> tmp(v.size());
-  for (int sh = 0; sh < 64 && (max_key >> sh); sh += 11) {
-    uint32_t cnt[2049] = {};
-    for (uint64_t e : v) ++cnt[((e >> sh) & 2047) + 1];
-    for (int i = 0; i < 2048; ++i) cnt[i + 1] += cnt[i];
-    for (uint64_t e : v) tmp[cnt[(e >> sh) & 2047]++] = e;
-    v.swap(tmp);
-  }
+// sorted candidates (pos << 1 | restart) -> first of each position
+__global__ __launch_bounds__(256) void unit_flags(const uint64_t *__restrict__ key, uint32_t cnt,
+                                                  uint32_t *__restrict__ flag) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i > cnt) return;
+  flag[i] = i < cnt && (i == 0 || (key[i] >> 1) != (key[i - 1] >> 1)) ? 1u : 0u;
+}
+
+// unit k + 1 starts at the k-th distinct sync point (unit 0 at `index`);
+// pos[cnt] = the number of distinct sync points
+__global__ __launch_bounds__(256) void unit_jobs(const uint64_t *__restrict__ key, const uint32_t *__restrict__ flag,
+                                                 const uint32_t *__restrict__ pos, uint32_t cnt, uint64_t n,
+                                                 uint64_t index, uint32_t cap, uint64_t *__restrict__ sync,
+                                                 uint8_t *__restrict__ restart, TokJob *__restrict__ jobs) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  auto job = [&](uint32_t u, uint64_t start) {
+    TokJob j;
+    j.start = start;
+    j.tok_off = (uint64_t)u * cap;
+    const uint64_t left = n - start;
+    j.tok_cap = (uint32_t)(left * 8 + 64 < cap ? left * 8 + 64 : cap);
+    j.stop_first = u;  // sync[u] is the first sync point after start
+    j.end = 0;
+    jobs[u] = j;
+  };
+  if (i == 0) job(0, index);
+  if (i >= cnt || !flag[i]) return;
+  const uint32_t k = pos[i];
+  const uint64_t p = key[i] >> 1;
+  sync[k] = p;
+  restart[k] = (uint8_t)(key[i] & 1);
+  job(k + 1, p);
 }
 
 }  // namespace
@@ -161,42 +185,47 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   ZT_HIP(hipMemcpyAsync(&cnt, d_count, 4, hipMemcpyDeviceToHost, s));
   ZT_HIP(hipStreamSynchronize(s));
   if (cnt == 0 || cnt > kMaxSync) FALLBACK("%u sync points\n", cnt);
-  // metadata moves through pinned staging (slot 1):
-  // [list | jobs | results | chain | segments | statuses]
-  void *hp;
+  // 2. the candidates sorted, deduplicated and turned into units on the
+  // device (hipcub radix sort + scan): unit 0 starts at `index`, unit k + 1
+  // at the k-th sync point
+  int end_bit = 1;
+  while (end_bit < 64 && ((uint64_t)n << 1 | 1) >> end_bit) ++end_bit;
+  size_t t_sort = 0, t_scan = 0;
+  ZT_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, t_sort, (const uint64_t *)nullptr, (uint64_t *)nullptr,
+                                           (int)cnt, 0, end_bit, s));
+  ZT_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, t_scan, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                          (int)cnt + 1, s));
+  const size_t t_bytes = align256(std::max(t_sort, t_scan));
+  const size_t key_bytes = align256((size_t)cnt * 8), flag_bytes = align256(((size_t)cnt + 1) * 4);
+  void *d_sort;
+  ZT_TRY(scratch(c, 20, t_bytes + key_bytes + 2 * flag_bytes, &d_sort));
+  uint8_t *sb = static_cast<uint8_t *>(d_sort);
+  uint64_t *d_key = reinterpret_cast<uint64_t *>(sb + t_bytes);
+  uint32_t *d_flag = reinterpret_cast<uint32_t *>(sb + t_bytes + key_bytes);
+  uint32_t *d_pos = reinterpret_cast<uint32_t *>(sb + t_bytes + key_bytes + flag_bytes);
+  ZT_HIP(hipcub::DeviceRadixSort::SortKeys(sb, t_sort, d_list, d_key, (int)cnt, 0, end_bit, s));
+  const uint32_t g = (cnt + 1 + 255) / 256;
+  unit_flags<<<g, 256, 0, s>>>(d_key, cnt, d_flag);
+  ZT_HIP(hipGetLastError());
+  ZT_HIP(hipcub::DeviceScan::ExclusiveSum(sb, t_scan, d_flag, d_pos, (int)cnt + 1, s));
   const size_t units_max = (size_t)cnt + 1;
-  const size_t meta_a = align256((size_t)cnt * 8) + align256(units_max * sizeof(TokJob)) +
-                        align256(units_max * sizeof(TokResult));
-  const size_t meta_b = align256(units_max * sizeof(ChainUnit)) + align256(units_max * sizeof(SegJob)) +
-                        2 * align256(units_max * 4);
-  ZT_TRY(pinned(c, meta_a + meta_b, &hp, 1));
-  uint8_t *pin = static_cast<uint8_t *>(hp);
-  ZT_HIP(hipMemcpyAsync(pin, d_list, (size_t)cnt * 8, hipMemcpyDeviceToHost, s));
+  const size_t stops_bytes = align256((size_t)cnt * 8);
+  const size_t restart_bytes = align256(units_max);
+  const size_t jobs_bytes = align256(units_max * sizeof(TokJob));
+  const size_t res_bytes = align256(units_max * sizeof(TokResult));
+  void *d_meta;
+  ZT_TRY(scratch(c, 6, stops_bytes + restart_bytes + jobs_bytes + res_bytes, &d_meta));
+  uint64_t *d_stops = static_cast<uint64_t *>(d_meta);
+  uint8_t *d_restart = static_cast<uint8_t *>(d_meta) + stops_bytes;
+  TokJob *d_jobs = reinterpret_cast<TokJob *>(static_cast<uint8_t *>(d_meta) + stops_bytes + restart_bytes);
+  TokResult *d_res =
+      reinterpret_cast<TokResult *>(static_cast<uint8_t *>(d_meta) + stops_bytes + restart_bytes + jobs_bytes);
+  unit_jobs<<<g, 256, 0, s>>>(d_key, d_flag, d_pos, cnt, n, index, kUnitTokCap, d_stops, d_restart, d_jobs);
+  ZT_HIP(hipGetLastError());
+  uint32_t nsync = 0;
+  ZT_HIP(hipMemcpyAsync(&nsync, d_pos + cnt, 4, hipMemcpyDeviceToHost, s));
   ZT_HIP(hipStreamSynchronize(s));
-  std::vector<uint64_t> raw(reinterpret_cast<uint64_t *>(pin), reinterpret_cast<uint64_t *>(pin) + cnt);
-  radix_sort(raw, (uint64_t)n << 1 | 1);
-  std::vector<uint64_t> sync;
-  std::vector<uint8_t> restart;
-  sync.reserve(raw.size());
-  restart.reserve(raw.size());
-  for (uint64_t e : raw) {
-    const uint64_t p = e >> 1;
-    if (!sync.empty() && sync.back() == p) continue;
-    sync.push_back(p);
-    restart.push_back((uint8_t)(e & 1));
-  }
-  // 2. units: the stream start and every sync point
-  const size_t units = sync.size() + 1;
-  std::vector<TokJob> jobs(units);
-  for (size_t i = 0; i < units; ++i) {
-    TokJob &j = jobs[i];
-    j.start = i ? sync[i - 1] : index;
-    j.tok_off = (uint64_t)i * kUnitTokCap;
-    const uint64_t left = n - j.start;
-    j.tok_cap = (uint32_t)std::min<uint64_t>(kUnitTokCap, left * 8 + 64);
-    j.stop_first = (uint32_t)i;  // sync[i] is the first sync point after start
-    j.end = 0;
-  }
+  const size_t units = (size_t)nsync + 1;
   // Every candidate sync point gets a token slot before the chain shows which
   // are real block boundaries, so a stream whose stored data is full of the
   // pattern (or whose tail holds further members) could ask for far more
@@ -204,24 +233,22 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   // slots cannot be allocated, the stream takes the one-wave path instead.
   const size_t tok_bytes = (units * (size_t)kUnitTokCap + 256) * 4;  // + slack: chunked token reads
   if (tok_bytes > 16 * (n - index) + (64u << 20)) FALLBACK("%zu sync candidates: token slots over budget\n", units);
-  void *d_tok, *d_meta;
+  void *d_tok;
   if (scratch(c, 4, tok_bytes, &d_tok) != ZT_OK) FALLBACK("token slots (%zu B) not allocated\n", tok_bytes);
-  const size_t stops_bytes = align256(sync.size() * 8);
-  const size_t jobs_bytes = align256(units * sizeof(TokJob));
-  const size_t res_bytes = align256(units * sizeof(TokResult));
-  ZT_TRY(scratch(c, 6, stops_bytes + jobs_bytes + res_bytes, &d_meta));
-  uint64_t *d_stops = static_cast<uint64_t *>(d_meta);
-  TokJob *d_jobs = reinterpret_cast<TokJob *>(static_cast<uint8_t *>(d_meta) + stops_bytes);
-  TokResult *d_res = reinterpret_cast<TokResult *>(static_cast<uint8_t *>(d_meta) + stops_bytes + jobs_bytes);
-  ZT_HIP(hipMemcpyAsync(d_stops, sync.data(), sync.size() * 8, hipMemcpyHostToDevice, s));
-  TokJob *h_jobs = reinterpret_cast<TokJob *>(pin + align256((size_t)cnt * 8));
-  memcpy(h_jobs, jobs.data(), units * sizeof(TokJob));
-  ZT_HIP(hipMemcpyAsync(d_jobs, h_jobs, units * sizeof(TokJob), hipMemcpyHostToDevice, s));
+  // metadata comes back through pinned staging (slot 1):
+  // [restart flags | results | chain | segments | statuses]
+  void *hp;
+  const size_t meta_a = restart_bytes + res_bytes;
+  const size_t meta_b = align256(units_max * sizeof(ChainUnit)) + align256(units_max * sizeof(SegJob)) +
+                        2 * align256(units_max * 4);
+  ZT_TRY(pinned(c, meta_a + meta_b, &hp, 1));
+  uint8_t *pin = static_cast<uint8_t *>(hp);
+  const uint8_t *restart = pin;
   TokParams tp;
   tp.in = d_in;
   tp.n = n;
   tp.stops = d_stops;
-  tp.nstops = sync.size();
+  tp.nstops = nsync;
   tp.jobs = d_jobs;
   tp.res = d_res;
   tp.tokens = static_cast<uint32_t *>(d_tok);
@@ -241,7 +268,8 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   ZT_TRY(timing_begin(c, s, 3));
   ZT_TRY(tokenize_units_dev(tp, s));
   ZT_TRY(timing_end(c, s, 3));
-  TokResult *res = reinterpret_cast<TokResult *>(pin + align256((size_t)cnt * 8) + align256(units_max * sizeof(TokJob)));
+  TokResult *res = reinterpret_cast<TokResult *>(pin + restart_bytes);
+  ZT_HIP(hipMemcpyAsync(pin, d_restart, nsync, hipMemcpyDeviceToHost, s));
   ZT_HIP(hipMemcpyAsync(res, d_res, units * sizeof(TokResult), hipMemcpyDeviceToHost, s));
   ZT_HIP(hipStreamSynchronize(s));
   if (check) {
@@ -279,9 +307,8 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   for (;;) {
     const TokResult &r = res[u];
     if (r.status != ZT_OK || r.out_len > 0xFFFFFFFFull)
-      FALLBACK("unit %zu (start %llu, chain %zu): status %d detail %d ntok %u out %llu\n", u,
-               (unsigned long long)jobs[u].start, chain.size(), r.status, r.detail, r.ntok,
-               (unsigned long long)r.out_len);
+      FALLBACK("unit %zu (chain %zu): status %d detail %d ntok %u out %llu\n", u, chain.size(), r.status,
+               r.detail, r.ntok, (unsigned long long)r.out_len);
     const bool seg_start_here = u == 0 || restart[u - 1];
     if (seg_start_here || segs.empty()) {
       desc_total = (desc_total + 511) & ~uint64_t(511);
@@ -289,7 +316,7 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
       seg_start = total;
       segs.push_back(SegJob{(uint32_t)chain.size(), 0});
     }
-    chain.push_back(ChainUnit{jobs[u].tok_off, total, seg_start, desc_seg + (total - seg_start), r.ntok,
+    chain.push_back(ChainUnit{(uint64_t)u * kUnitTokCap, total, seg_start, desc_seg + (total - seg_start), r.ntok,
                               (uint32_t)r.out_len});
     segs.back().count++;
     total += r.out_len;

@@ -44,8 +44,9 @@ struct DeviceCtx {
   uint32_t *d_crc_x2n = nullptr;    // x^(2^k) mod P, k = 0..31
   uint32_t *d_crc_shift = nullptr;  // checksum.hip merge constants (crc_shift_tables)
   // scratch
-  void *d_buf[20] = {};  // slot 8: checksum segment partials; 10-17: general inflate (inflate_gen.hip)
-  size_t buf_size[20] = {};
+  void *d_buf[21] = {};  // slot 8: checksum segment partials; 10-17: general inflate (inflate_gen.hip);
+                         // 20: segment inflate's sync-point sort (inflate_seg.hip)
+  size_t buf_size[21] = {};
   // second stream: checksums run beside the deflate pipeline in the containers
   hipStream_t aux = nullptr;
   hipEvent_t aux_ev = nullptr;
