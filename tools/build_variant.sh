@@ -5,7 +5,7 @@
 set -e
 NAME=$1; shift
 cd "$(dirname "$0")/../zlib.ts_amd"
-OUT=build/var_$NAME; mkdir -p $OUT
+OUT=build/${VAR_PREFIX:-var_}$NAME; mkdir -p $OUT
 for f in csrc/*.hip csrc/*.cpp; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-function "$@" -c -o $OUT/$(basename $f).o $f &
 done

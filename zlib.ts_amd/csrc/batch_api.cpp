@@ -40,7 +40,7 @@ struct Framing {
 int frame_item(const Framing &fr, size_t n_in, const uint8_t *body, size_t blen, uint32_t crc, uint32_t adler,
                uint8_t **out, size_t *out_len) {
   const size_t total = fr.prefix.size() + blen + fr.trailer;
-  uint8_t *h = (uint8_t *)malloc(total ? total : 1);
+  uint8_t *h = host_out(total);
   if (!h) return set_error(ZT_E_NOMEM, "host allocation failed");
   if (!fr.prefix.empty()) memcpy(h, fr.prefix.data(), fr.prefix.size());
   if (blen) memcpy(h + fr.prefix.size(), body, blen);

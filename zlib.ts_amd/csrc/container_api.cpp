@@ -70,7 +70,7 @@ int deflate_with_checksums(const uint8_t *in, size_t n, const zt_deflate_opts *o
   }
   size_t len = 0;
   ZT_TRY(deflate_dev_run(c, (const uint8_t *)d_in, n, 0, 1, ct, lv, (uint8_t *)d_out, &len, d_scr, ss, c->stream));
-  uint8_t *h = (uint8_t *)malloc(prefix_len + len + trailer + 1);
+  uint8_t *h = host_out(prefix_len + len + trailer + 1);
   if (!h) return set_error(ZT_E_NOMEM, "host allocation failed");
   if (prefix_len) memcpy(h, prefix, prefix_len);
   if (const int rc = download(c, h + prefix_len, d_out, len, c->stream)) {
@@ -273,7 +273,7 @@ int zt_gunzip(const uint8_t *in, size_t n, uint8_t **out, size_t *out_len, zt_gz
     mem.push_back(m);
     ip = t.p;
   }
-  uint8_t *h = (uint8_t *)malloc(data.size() ? data.size() : 1);
+  uint8_t *h = host_out(data.size());
   if (!h) return set_error(ZT_E_NOMEM, "host allocation failed");
   if (!data.empty()) memcpy(h, data.data(), data.size());
   *out = h;

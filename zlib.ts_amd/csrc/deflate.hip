@@ -1971,6 +1971,10 @@ static uint32_t restart_blocks() {
   return e >= 4 ? (uint32_t)e : kRestartBlocks;
 }
 
+// bytes per independent segment: a deflate call on a slice that starts at a
+// multiple of it (halo 0) writes that slice's part of the whole-buffer stream
+size_t deflate_segment_bytes() { return (size_t)restart_blocks() * DF_BLOCK; }
+
 size_t deflate_bound_bytes(size_t n) {
   size_t nb = (n + DF_BLOCK - 1) / DF_BLOCK;
   return n + nb * 16 + (nb / 4 + 1) * kRestartMarkerLen + 64;

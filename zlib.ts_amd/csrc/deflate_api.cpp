@@ -1,5 +1,6 @@
 // deflate_api.cpp -- host side of the deflate entry points and the
 // device-resident plans (include/zt.h).
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -9,6 +10,7 @@
 namespace zt {
 
 size_t deflate_bound_bytes(size_t n);
+size_t deflate_segment_bytes();
 size_t deflate_scratch_bytes(const DeviceCtx *c, size_t n);
 int deflate_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t halo, int final_, int ctype, int level,
                     uint8_t *d_out, size_t *out_len, void *scratch_base, size_t scratch_size, hipStream_t s);
@@ -95,6 +97,56 @@ int zt_deflate_dev(zt_deflate_plan *plan, const void *d_in, size_t n, size_t hal
                          out_len, plan->scratch, plan->scratch_size, s);
 }
 
+// Large host inputs (zt_deflate_raw): PCIe overlapped with the deflate.
+// The input is cut into pieces at segment boundaries (restart points, 1 MiB);
+// piece i + 1 is uploaded while piece i is deflated and piece i - 1's stream
+// comes back (pipeline_h2d_d2h).  A piece deflated with halo 0 and BFINAL
+// only on the last one writes exactly its part of the single-call stream (no
+// match crosses a restart point; a non-final piece ends with the restart
+// marker), so the result is byte-identical to the unpipelined call
+// (tests/test_gpu_api_pipeline.py).  Pieces of n / 8 (32-128 MiB) keep >= 2
+// match workgroups per CU and bound the fill / drain to one piece.
+static constexpr size_t kPipeMin = 64u << 20;
+
+static int deflate_raw_pipelined(DeviceCtx *c, const uint8_t *in, size_t n, int ct, int lv, uint8_t **out,
+                                 size_t *out_len) {
+  const size_t seg = deflate_segment_bytes();
+  size_t piece = std::min(std::max(n / 8, (size_t)32 << 20), (size_t)128 << 20);
+  piece = (piece + seg - 1) / seg * seg;
+  const size_t np = (n + piece - 1) / piece;
+  const size_t pb = (out_bound(ct, piece) + 255) & ~(size_t)255;
+  void *d_in, *d_out, *d_scr;
+  ZT_TRY(scratch(c, 0, n + 64, &d_in));
+  ZT_TRY(scratch(c, 1, pb * np, &d_out));
+  const size_t ss = deflate_scratch_bytes(c, piece);
+  ZT_TRY(scratch(c, 3, ss, &d_scr));
+  uint8_t *h = host_out(pb * np);
+  if (!h) return set_error(ZT_E_NOMEM, "host allocation failed");
+  size_t total = 0;
+  const int rc = pipeline_h2d_d2h(
+      c, np,
+      [&](size_t i) {
+        const size_t off = i * piece;
+        return PipePiece{in + off, (uint8_t *)d_in + off, std::min(piece, n - off)};
+      },
+      [&](size_t i, const void **d_res, size_t *n_res) -> int {
+        const size_t off = i * piece;
+        uint8_t *d_o = (uint8_t *)d_out + i * pb;
+        ZT_TRY(deflate_dev_run(c, (const uint8_t *)d_in + off, std::min(piece, n - off), 0, i + 1 == np, ct, lv, d_o,
+                               n_res, d_scr, ss, c->stream));
+        *d_res = d_o;
+        return ZT_OK;
+      },
+      h, pb * np, &total);
+  if (rc) {
+    free(h);
+    return rc;
+  }
+  *out = h;  // (its pages past the stream were never touched)
+  *out_len = total;
+  return ZT_OK;
+}
+
 int zt_deflate_raw(const uint8_t *in, size_t n, const zt_deflate_opts *opts, uint8_t **out, size_t *out_len) {
   if (!out || !out_len) return set_error(ZT_E_ARG, "null output");
   if (n && !in) return set_error(ZT_E_ARG, "null input");
@@ -103,6 +155,7 @@ int zt_deflate_raw(const uint8_t *in, size_t n, const zt_deflate_opts *opts, uin
   std::lock_guard<std::recursive_mutex> ctx_lock(c->mu);
   int ct, lv;
   ZT_TRY(resolve(opts, &ct, &lv));
+  if (ct != 0 && n >= kPipeMin) return deflate_raw_pipelined(c, in, n, ct, lv, out, out_len);
   const size_t ob = out_bound(ct, n);
   void *d_in, *d_out, *d_scr;
   ZT_TRY(scratch(c, 0, n + 64, &d_in));
@@ -112,7 +165,7 @@ int zt_deflate_raw(const uint8_t *in, size_t n, const zt_deflate_opts *opts, uin
   ZT_TRY(upload(c, d_in, in, n, c->stream));
   size_t len = 0;
   ZT_TRY(deflate_dev_run(c, (const uint8_t *)d_in, n, 0, 1, ct, lv, (uint8_t *)d_out, &len, d_scr, ss, c->stream));
-  uint8_t *h = (uint8_t *)malloc(len ? len : 1);
+  uint8_t *h = host_out(len);
   if (!h) return set_error(ZT_E_NOMEM, "host allocation failed");
   const int rc = download(c, h, d_out, len, c->stream);
   if (rc) {

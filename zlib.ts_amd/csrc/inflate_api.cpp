@@ -319,7 +319,7 @@ int inflate_dev_member(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t index
       if (seg == 1) seg = inflate_general_dev(c, d_in, ne, index, &d_out, 0, &ol, &eip, s);
       if (seg < 0) return seg;
       if (seg == 0) {
-        uint8_t *h = (uint8_t *)malloc(ol ? ol : 1);
+        uint8_t *h = host_out(ol);
         if (!h) return set_error(ZT_E_NOMEM, "host allocation failed");
         const int rc = download(c, h, d_out, ol, s);
         if (rc) {
@@ -363,7 +363,7 @@ int zt_inflate_raw(const uint8_t *in, size_t n, size_t index, const zt_inflate_o
     if (seg == 1) seg = inflate_general_dev(c, (const uint8_t *)d_in, n, index, &d_out, 0, &ol, &eip, c->stream);
     if (seg < 0) return seg;
     if (seg == 0) {
-      uint8_t *h = (uint8_t *)malloc(ol ? ol : 1);
+      uint8_t *h = host_out(ol);
       if (!h) return set_error(ZT_E_NOMEM, "host allocation failed");
       const int rc = download(c, h, d_out, ol, c->stream);
       if (rc) {
@@ -445,7 +445,7 @@ int zt_inflate_raw_resume(const uint8_t *in, size_t n, uint64_t bit_pos, const u
       cap = (size_t)done;
       continue;
     }
-    uint8_t *h = (uint8_t *)malloc(done ? done : 1);
+    uint8_t *h = host_out(done);
     if (!h) return set_error(ZT_E_NOMEM, "host allocation failed");
     const int rc = download(c, h, d_out, done, c->stream);
     if (rc) {

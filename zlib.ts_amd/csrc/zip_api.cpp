@@ -170,7 +170,7 @@ int zt_zip_compress(const uint8_t *const *in, const size_t *n, const zt_zip_file
   put16(eo, (uint32_t)comment_len);
   if (comment_len) eo.insert(eo.end(), comment, comment + comment_len);
   const size_t total = lo.size() + cd.size() + eo.size();
-  uint8_t *h = (uint8_t *)malloc(total);
+  uint8_t *h = host_out(total);
   if (!h) return set_error(ZT_E_NOMEM, "host allocation failed");
   memcpy(h, lo.data(), lo.size());
   memcpy(h + lo.size(), cd.data(), cd.size());
@@ -320,7 +320,7 @@ int zt_unzip(const uint8_t *in, size_t n, int verify, uint8_t **out, size_t *out
   // the output: every entry's data, concatenated
   size_t tot = 0;
   for (uint32_t i = 0; i < total; ++i) tot += ol[i];
-  uint8_t *h = (uint8_t *)malloc(tot ? tot : 1);
+  uint8_t *h = host_out(tot);
   if (!h) return set_error(ZT_E_NOMEM, "host allocation failed");
   size_t p = 0;
   std::vector<const uint8_t *> cp;

@@ -2,7 +2,10 @@
 //
 // Every entry point computes on the GPU.  There is deliberately no CPU
 // fallback: without a HIP device the calls fail with ZT_E_NO_DEVICE.
+#include <sys/mman.h>
+
 #include <algorithm>
+#include <condition_variable>
 #include <functional>
 #include <thread>
 #include <cstdio>
@@ -106,6 +109,17 @@ int scratch(DeviceCtx *c, int slot, size_t bytes, void **ptr) {
   return ZT_OK;
 }
 
+uint8_t *host_out(size_t n) {
+  if (n < (8u << 20)) return (uint8_t *)malloc(n ? n : 1);
+  // large outputs: 2 MiB-aligned and backed by transparent huge pages where
+  // the kernel allows it -- 512x fewer first-touch faults while the
+  // download fills them (freed by zt_free = free)
+  void *p = nullptr;
+  if (posix_memalign(&p, 2u << 20, n)) return nullptr;
+  (void)madvise(p, n, MADV_HUGEPAGE);
+  return (uint8_t *)p;
+}
+
 int pinned(DeviceCtx *c, size_t bytes, void **ptr, int slot) {
   if (bytes == 0) bytes = 16;
   if (c->pinned_size[slot] < bytes) {
@@ -129,8 +143,10 @@ int pinned(DeviceCtx *c, size_t bytes, void **ptr, int slot) {
 // the PCIe rate.  Buffers below 8 MiB are copied directly.
 static constexpr size_t kXferChunk = 32u << 20;
 
+// (fresh output pages fault in during the copy: 8 threads keep a 32 MiB
+// chunk's faults and copy under its DMA time; tools/micro/host_fault_probe)
 static void host_copy(void *dst, const void *src, size_t n) {
-  const size_t nt = n >= (8u << 20) ? 4 : 1;
+  const size_t nt = n >= (16u << 20) ? 8 : n >= (8u << 20) ? 4 : 1;
   if (nt == 1) {
     memcpy(dst, src, n);
     return;
@@ -196,6 +212,142 @@ int download(DeviceCtx *c, void *h_dst, const void *d_src, size_t n, hipStream_t
     const size_t off = k * kXferChunk, len = std::min(kXferChunk, n - off);
     host_copy((uint8_t *)h_dst + off, buf[k & 1], len);
   }
+  return ZT_OK;
+}
+
+// pipeline_h2d_d2h (zt_internal.h).  Each stage runs in order over the
+// pieces; the stages hand pieces on through counters under one mutex, and a
+// failing stage stops the others (its error text is re-raised on the
+// caller's thread, where zt_last_error_message() reads it).
+int pipeline_h2d_d2h(DeviceCtx *c, size_t np, const std::function<PipePiece(size_t)> &input,
+                     const std::function<int(size_t, const void **d_res, size_t *n_res)> &compute, uint8_t *out_base,
+                     size_t out_cap, size_t *out_total) {
+  if (!c->up) ZT_HIP(hipStreamCreateWithFlags(&c->up, hipStreamNonBlocking));
+  if (!c->dn) ZT_HIP(hipStreamCreateWithFlags(&c->dn, hipStreamNonBlocking));
+  uint8_t *stage[4];
+  for (int k = 0; k < 4; ++k) {
+    void *p;
+    ZT_TRY(pinned(c, kXferChunk, &p, 2 + k));
+    stage[k] = static_cast<uint8_t *>(p);
+    if (!c->xfer_ev[k]) ZT_HIP(hipEventCreateWithFlags(&c->xfer_ev[k], hipEventDisableTiming));
+  }
+  std::vector<hipEvent_t> landed(np, nullptr);
+  struct EvFree {
+    std::vector<hipEvent_t> &v;
+    ~EvFree() {
+      for (auto e : v)
+        if (e) (void)hipEventDestroy(e);
+    }
+  } ev_free{landed};
+  for (auto &e : landed) ZT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+
+  std::mutex mu;
+  std::condition_variable cv;
+  size_t uploaded = 0, computed = 0;  // pieces whose upload is enqueued / whose result is on the device
+  std::vector<const void *> res(np, nullptr);
+  std::vector<size_t> res_n(np, 0);
+  int err = 0;
+  std::string err_msg;
+  auto fail = [&](int rc) {
+    std::lock_guard<std::mutex> lk(mu);
+    if (!err) {
+      err = rc;
+      err_msg = zt_last_error_message();
+    }
+    cv.notify_all();
+  };
+  auto failed = [&] {
+    std::lock_guard<std::mutex> lk(mu);
+    return err != 0;
+  };
+  const int dev = c->device;
+  // stage 1: host -> pinned chunk (host threads) -> device (DMA on c->up)
+  auto up_stage = [&]() -> int {
+    ZT_HIP(hipSetDevice(dev));
+    size_t k = 0;  // chunks issued
+    for (size_t i = 0; i < np && !failed(); ++i) {
+      const PipePiece pc = input(i);
+      for (size_t off = 0; off < pc.n; off += kXferChunk, ++k) {
+        const size_t len = std::min(kXferChunk, pc.n - off);
+        if (k >= 2) ZT_HIP(hipEventSynchronize(c->xfer_ev[k & 1]));
+        host_copy(stage[k & 1], (const uint8_t *)pc.h_src + off, len);
+        ZT_HIP(hipMemcpyAsync((uint8_t *)pc.d_dst + off, stage[k & 1], len, hipMemcpyHostToDevice, c->up));
+        ZT_HIP(hipEventRecord(c->xfer_ev[k & 1], c->up));
+      }
+      ZT_HIP(hipEventRecord(landed[i], c->up));
+      std::lock_guard<std::mutex> lk(mu);
+      uploaded = i + 1;
+      cv.notify_all();
+    }
+    ZT_HIP(hipStreamSynchronize(c->up));  // the staging chunks are reused by the next call
+    return ZT_OK;
+  };
+  // stage 3: device -> pinned chunk (DMA on c->dn) -> host (host threads)
+  size_t total = 0;
+  auto dn_stage = [&]() -> int {
+    ZT_HIP(hipSetDevice(dev));
+    size_t k = 0;
+    for (size_t i = 0; i < np; ++i) {
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return computed > i || err; });
+        if (err) return ZT_OK;
+      }
+      const size_t n = res_n[i];
+      if (total + n > out_cap) return set_error(ZT_E_ARG, "pipeline output larger than its bound");
+      // chunks of this piece: issue k + 1 before copying k out of its staging buffer
+      const size_t nch = (n + kXferChunk - 1) / kXferChunk;
+      auto issue = [&](size_t j) -> int {
+        const size_t off = j * kXferChunk, len = std::min(kXferChunk, n - off);
+        ZT_HIP(hipMemcpyAsync(stage[2 + ((k + j) & 1)], (const uint8_t *)res[i] + off, len, hipMemcpyDeviceToHost,
+                              c->dn));
+        ZT_HIP(hipEventRecord(c->xfer_ev[2 + ((k + j) & 1)], c->dn));
+        return ZT_OK;
+      };
+      if (nch) ZT_TRY(issue(0));
+      for (size_t j = 0; j < nch; ++j) {
+        if (j + 1 < nch) ZT_TRY(issue(j + 1));
+        ZT_HIP(hipEventSynchronize(c->xfer_ev[2 + ((k + j) & 1)]));
+        const size_t off = j * kXferChunk, len = std::min(kXferChunk, n - off);
+        host_copy(out_base + total + off, stage[2 + ((k + j) & 1)], len);
+      }
+      k += nch;
+      total += n;
+    }
+    return ZT_OK;
+  };
+  std::thread tu([&] {
+    if (int rc = up_stage()) fail(rc);
+  });
+  std::thread td([&] {
+    if (int rc = dn_stage()) fail(rc);
+  });
+  // stage 2 on the caller's thread: compute(i) after piece i has landed
+  for (size_t i = 0; i < np; ++i) {
+    {
+      std::unique_lock<std::mutex> lk(mu);
+      cv.wait(lk, [&] { return uploaded > i || err; });
+      if (err) break;
+    }
+    int rc = hipStreamWaitEvent(c->stream, landed[i], 0) == hipSuccess ? ZT_OK
+                                                                       : set_error(ZT_E_HIP, "hipStreamWaitEvent");
+    const void *d = nullptr;
+    size_t m = 0;
+    if (!rc) rc = compute(i, &d, &m);
+    if (rc) {
+      fail(rc);
+      break;
+    }
+    std::lock_guard<std::mutex> lk(mu);
+    res[i] = d;
+    res_n[i] = m;
+    computed = i + 1;
+    cv.notify_all();
+  }
+  tu.join();
+  td.join();
+  if (err) return set_error(err, err_msg);
+  *out_total = total;
   return ZT_OK;
 }
 

@@ -50,13 +50,15 @@ struct DeviceCtx {
   // second stream: checksums run beside the deflate pipeline in the containers
   hipStream_t aux = nullptr;
   hipEvent_t aux_ev = nullptr;
-  void *h_pinned[4] = {};  // pinned host staging: 0 batch data, 1 inflate metadata, 2-3 upload/download chunks
-  hipEvent_t xfer_ev[2] = {};  // upload / download: chunk buffer k's copy has finished
+  void *h_pinned[6] = {};  // pinned host staging: 0 batch data, 1 inflate metadata, 2-3 upload/download chunks,
+                           // 4-5 download chunks of the three-stage pipeline (pipeline_h2d_d2h)
+  hipEvent_t xfer_ev[4] = {};  // chunk buffer 2 + k's copy has finished
+  hipStream_t up = nullptr, dn = nullptr;  // pipeline_h2d_d2h: H2D and D2H copy streams
   // zt_timing_enable: HIP-event kernel timing
   bool timing = false;
   hipEvent_t ev[8] = {};  // [2k, 2k+1]: interval k (0 match, 1 deflate pipeline, 2 inflate)
   zt_kernel_times times = {};
-  size_t pinned_size[4] = {};
+  size_t pinned_size[6] = {};
 };
 
 // Records the begin / end event of interval k (0 or 1) when timing is on.
@@ -71,6 +73,8 @@ int get_ctx(DeviceCtx **out);
 int scratch(DeviceCtx *c, int slot, size_t bytes, void **ptr);
 // Grow-only pinned host staging buffer `slot` (0 or 1) of at least `bytes`.
 int pinned(DeviceCtx *c, size_t bytes, void **ptr, int slot = 0);
+// Host output buffer the caller frees with zt_free (large ones on huge pages).
+uint8_t *host_out(size_t n);
 // fn(0 .. count-1) over a few host threads when total_bytes is large.
 void parallel_copy(size_t count, const std::function<void(size_t)> &fn, size_t total_bytes);
 
@@ -313,6 +317,20 @@ int inflate_dev_member(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t index
 int upload(DeviceCtx *c, void *d_dst, const void *h_src, size_t n, hipStream_t s);
 // device -> host, the same way; returns after the bytes are in h_dst
 int download(DeviceCtx *c, void *h_dst, const void *d_src, size_t n, hipStream_t s);
+// Three-stage host pipeline over np pieces, three engines busy at once: piece
+// i + 1 crosses PCIe to the device (pinned chunks, stream c->up, one host
+// thread) while compute(i) runs on the caller's thread (after piece i's upload
+// has landed; it returns the device bytes of its result) and piece i - 1's
+// result comes back (pinned chunks, stream c->dn, one host thread) to
+// out_base + the sum of the earlier results' lengths (out_cap bytes in all).
+struct PipePiece {
+  const void *h_src;  // host bytes of piece i
+  void *d_dst;        // where they go on the device
+  size_t n;
+};
+int pipeline_h2d_d2h(DeviceCtx *c, size_t np, const std::function<PipePiece(size_t)> &input,
+                     const std::function<int(size_t, const void **d_res, size_t *n_res)> &compute, uint8_t *out_base,
+                     size_t out_cap, size_t *out_total);
 int inflate_error(int status, int detail);
 
 }  // namespace zt
