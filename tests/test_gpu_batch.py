@@ -109,3 +109,37 @@ def test_set_devices(zt, oracle):
         assert zlib.decompress(m, 31) == f
     with pytest.raises(zt.ZtError):
         zt.set_devices(1 << n)
+
+
+@pytest.mark.parametrize("kind", ["gzip", "zlib"])
+def test_grouped_batch_equals_single_pipeline(zt, kind):
+    """A batch of >= 256 MiB runs as a grouped three-stage pipeline
+    (batch_api.cpp batch_grouped); every member must equal the one the single
+    pipeline writes for the same file (two halves of the batch, each below
+    the threshold) and decode to its input (Python zlib, independent)."""
+    import random
+    import zlib
+
+    import torch
+
+    rng = random.Random(5)
+    sizes = []
+    while sum(sizes) < (300 << 20):
+        sizes.append(int(2 ** rng.uniform(10, 21)) + rng.randrange(7))
+    total = sum(sizes)
+    d = torch.empty(total, dtype=torch.uint8, device="cuda")
+    zt.synth_dev("mixed", 9, d.data_ptr(), total)
+    host = d.cpu().numpy().tobytes()
+    files, o = [], 0
+    for s in sizes:
+        files.append(host[o:o + s])
+        o += s
+    fn = zt.gzip_compress_batch if kind == "gzip" else zt.zlib_compress_batch
+    whole = fn(files)
+    half = len(files) // 2
+    parts = fn(files[:half]) + fn(files[half:])
+    assert len(whole) == len(files)
+    assert whole == parts
+    for f, mb in zip(files[::97], whole[::97]):
+        dec = zlib.decompress(mb, 31 if kind == "gzip" else 15)
+        assert dec == f

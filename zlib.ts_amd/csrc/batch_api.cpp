@@ -14,8 +14,10 @@
 // new Deflate(input).compress() (src/Deflate.ts:60-99) and
 // new RawDeflate(input).compress() (src/RawDeflate.ts:87-114).
 #include <algorithm>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -56,6 +58,174 @@ int frame_item(const Framing &fr, size_t n_in, const uint8_t *body, size_t blen,
   return ZT_OK;
 }
 
+// Large shares (>= kGroupMin padded bytes): the items are cut, in order, into
+// groups of about 1/6 of the share (>= 128 MiB) and run as a three-stage
+// pipeline, so PCIe and the host work overlap the GPU: group g + 1 is packed
+// into pinned staging and uploaded (stream c->up, one host thread) while
+// group g is checksummed (c->aux) and deflated (c->stream, the caller's
+// thread) and group g - 1 comes back and is framed into the members (stream
+// c->dn, one host thread).  Groups are independent batch pipelines (no item
+// spans two), so every member is the one the single pipeline writes.
+constexpr uint64_t kGroupMin = 256ull << 20;
+
+int batch_grouped(DeviceCtx *c, const uint8_t *const *in, const std::vector<size_t> &work,
+                  const std::vector<uint64_t> &off, const std::vector<uint64_t> &len, uint64_t padded, int ct, int lv,
+                  const Framing &fr, uint8_t **out, size_t *out_len) {
+  const size_t m = work.size();
+  const bool sums = fr.kind != Framing::RAW;
+  // groups [gk[g], gk[g + 1]) of items
+  // tuning hook: ZT_BATCH_GROUPS = groups per share (default 6)
+  static const int ng_env = getenv("ZT_BATCH_GROUPS") ? atoi(getenv("ZT_BATCH_GROUPS")) : 0;
+  const uint64_t target = std::max<uint64_t>(padded / (ng_env > 0 ? ng_env : 6), 64ull << 20);
+  std::vector<size_t> gk{0};
+  for (size_t k = 0; k < m; ++k)
+    if (k + 1 < m && off[k + 1] - off[gk.back()] >= target) gk.push_back(k + 1);
+  gk.push_back(m);
+  const size_t ng = gk.size() - 1;
+  auto gbeg = [&](size_t g) { return off[gk[g]]; };
+  auto gend = [&](size_t g) { return gk[g + 1] < m ? off[gk[g + 1]] : padded; };
+  auto obound = [](uint64_t p) { return (p + p / 8 + 1024 * (p / kBlk + 1) + 4096 + 255) & ~uint64_t(255); };
+  uint64_t gmax = 0, obmax = 0, obsum = 0;
+  std::vector<uint64_t> ooff(ng + 1, 0);  // device output region of group g
+  for (size_t g = 0; g < ng; ++g) {
+    gmax = std::max(gmax, gend(g) - gbeg(g));
+    obmax = std::max(obmax, obound(gend(g) - gbeg(g)));
+    ooff[g + 1] = ooff[g] + obound(gend(g) - gbeg(g));
+  }
+  obsum = ooff[ng];
+  void *d_in, *d_out, *d_scr, *d_sums = nullptr, *p;
+  ZT_TRY(scratch(c, 0, padded + 64, &d_in));
+  ZT_TRY(scratch(c, 1, obsum, &d_out));
+  const size_t ss = deflate_batch_scratch_bytes(c, gmax);
+  ZT_TRY(scratch(c, 3, ss, &d_scr));
+  if (sums) ZT_TRY(scratch(c, 18, 8 * m, &d_sums));
+  uint8_t *stage_in[2], *stage_out;
+  ZT_TRY(pinned(c, gmax, &p, 0));
+  stage_in[0] = static_cast<uint8_t *>(p);
+  ZT_TRY(pinned(c, gmax, &p, 6));
+  stage_in[1] = static_cast<uint8_t *>(p);
+  ZT_TRY(pinned(c, obmax, &p, 7));
+  stage_out = static_cast<uint8_t *>(p);
+  if (!c->up) ZT_HIP(hipStreamCreateWithFlags(&c->up, hipStreamNonBlocking));
+  if (!c->dn) ZT_HIP(hipStreamCreateWithFlags(&c->dn, hipStreamNonBlocking));
+  std::vector<hipEvent_t> landed(ng, nullptr), staged(2, nullptr);
+  struct EvFree {
+    std::vector<hipEvent_t> &a, &b;
+    ~EvFree() {
+      for (auto e : a)
+        if (e) (void)hipEventDestroy(e);
+      for (auto e : b)
+        if (e) (void)hipEventDestroy(e);
+    }
+  } ev_free{landed, staged};
+  for (auto &e : landed) ZT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  for (auto &e : staged) ZT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+
+  std::vector<uint32_t> hsums(2 * m, 0);
+  std::vector<uint64_t> oo(m + ng, 0);  // group g's stream offsets at oo[gk[g] + g ..]
+  std::mutex mu;
+  std::condition_variable cv;
+  size_t uploaded = 0, computed = 0;
+  int err = 0;
+  std::string err_msg;
+  auto fail = [&](int rc) {
+    std::lock_guard<std::mutex> lk(mu);
+    if (!err) {
+      err = rc;
+      err_msg = zt_last_error_message();
+    }
+    cv.notify_all();
+  };
+  auto wait_for = [&](const size_t &counter, size_t g) {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&] { return counter > g || err; });
+    return err == 0;
+  };
+  const int dev = c->device;
+  auto up_stage = [&]() -> int {
+    ZT_HIP(hipSetDevice(dev));
+    for (size_t g = 0; g < ng; ++g) {
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        if (err) return ZT_OK;
+      }
+      uint8_t *st = stage_in[g & 1];
+      if (g >= 2) ZT_HIP(hipEventSynchronize(staged[g & 1]));  // its previous upload has left
+      const uint64_t b = gbeg(g), nb = gk[g + 1] - gk[g];
+      parallel_copy(nb, [&](size_t j) {
+        const size_t k = gk[g] + j;
+        memcpy(st + off[k] - b, in[work[k]], len[k]);
+        memset(st + off[k] - b + len[k], 0, round_blk(len[k]) - len[k]);
+      }, gend(g) - b);
+      ZT_HIP(hipMemcpyAsync((uint8_t *)d_in + b, st, gend(g) - b, hipMemcpyHostToDevice, c->up));
+      ZT_HIP(hipEventRecord(staged[g & 1], c->up));
+      ZT_HIP(hipEventRecord(landed[g], c->up));
+      std::lock_guard<std::mutex> lk(mu);
+      uploaded = g + 1;
+      cv.notify_all();
+    }
+    ZT_HIP(hipStreamSynchronize(c->up));
+    return ZT_OK;
+  };
+  auto dn_stage = [&]() -> int {
+    ZT_HIP(hipSetDevice(dev));
+    for (size_t g = 0; g < ng; ++g) {
+      if (!wait_for(computed, g)) return ZT_OK;
+      const size_t k0 = gk[g], nb = gk[g + 1] - k0;
+      const uint64_t *go = &oo[k0 + g];
+      ZT_HIP(hipMemcpyAsync(stage_out, (uint8_t *)d_out + ooff[g], go[nb], hipMemcpyDeviceToHost, c->dn));
+      ZT_HIP(hipStreamSynchronize(c->dn));
+      std::vector<int> rcs(nb, ZT_OK);
+      parallel_copy(nb, [&](size_t j) {
+        const size_t k = k0 + j, i = work[k];
+        rcs[j] = frame_item(fr, len[k], stage_out + go[j], go[j + 1] - go[j], hsums[2 * k], hsums[2 * k + 1], &out[i],
+                            &out_len[i]);
+      }, go[nb]);
+      for (int rc : rcs)
+        if (rc) return rc;
+    }
+    return ZT_OK;
+  };
+  std::thread tu([&] {
+    if (int rc = up_stage()) fail(rc);
+  });
+  std::thread td([&] {
+    if (int rc = dn_stage()) fail(rc);
+  });
+  for (size_t g = 0; g < ng; ++g) {
+    if (!wait_for(uploaded, g)) break;
+    const size_t k0 = gk[g], nb = gk[g + 1] - k0;
+    const uint64_t b = gbeg(g);
+    std::vector<uint64_t> ro(nb), rl(len.begin() + k0, len.begin() + k0 + nb);
+    for (size_t j = 0; j < nb; ++j) ro[j] = off[k0 + j] - b;
+    auto step = [&]() -> int {
+      ZT_HIP(hipStreamWaitEvent(c->stream, landed[g], 0));
+      if (sums) {
+        ZT_HIP(hipStreamWaitEvent(c->aux, landed[g], 0));
+        ZT_TRY(checksums_batch_dev(c, (const uint8_t *)d_in + b, nb, ro.data(), rl.data(),
+                                   (uint32_t *)d_sums + 2 * k0, c->aux));
+        ZT_HIP(hipMemcpyAsync(hsums.data() + 2 * k0, (uint32_t *)d_sums + 2 * k0, 8 * nb, hipMemcpyDeviceToHost,
+                              c->aux));
+      }
+      ZT_TRY(deflate_batch_dev_run(c, (const uint8_t *)d_in + b, nb, ro.data(), rl.data(), ct, lv,
+                                   (uint8_t *)d_out + ooff[g], &oo[k0 + g], d_scr, ss, c->stream));
+      if (sums) ZT_HIP(hipStreamSynchronize(c->aux));
+      return ZT_OK;
+    };
+    if (int rc = step()) {
+      fail(rc);
+      break;
+    }
+    std::lock_guard<std::mutex> lk(mu);
+    computed = g + 1;
+    cv.notify_all();
+  }
+  tu.join();
+  td.join();
+  if (err) return set_error(err, err_msg);
+  return ZT_OK;
+}
+
 // one device's share: items `ids` of the batch
 int batch_on_device(int dev, const uint8_t *const *in, const size_t *n, const std::vector<size_t> &ids, int ct,
                     int lv, const Framing &fr, uint8_t **out, size_t *out_len, std::string *err) {
@@ -89,6 +259,10 @@ int batch_on_device(int dev, const uint8_t *const *in, const size_t *n, const st
     len[k] = n[work[k]];
     padded += round_blk(len[k]);
     in_bytes += len[k];
+  }
+  if (ct != 0 && padded >= kGroupMin && m >= 2) {
+    const int rc = batch_grouped(c, in, work, off, len, padded, ct, lv, fr, out, out_len);
+    return rc ? fail(rc) : ZT_OK;
   }
   void *d_in, *h_stage;
   if (int rc = scratch(c, 0, padded + 64, &d_in)) return fail(rc);

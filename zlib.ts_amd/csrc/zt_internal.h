@@ -50,15 +50,16 @@ struct DeviceCtx {
   // second stream: checksums run beside the deflate pipeline in the containers
   hipStream_t aux = nullptr;
   hipEvent_t aux_ev = nullptr;
-  void *h_pinned[6] = {};  // pinned host staging: 0 batch data, 1 inflate metadata, 2-3 upload/download chunks,
-                           // 4-5 download chunks of the three-stage pipeline (pipeline_h2d_d2h)
+  void *h_pinned[8] = {};  // pinned host staging: 0 batch data, 1 inflate metadata, 2-3 upload/download chunks,
+                           // 4-5 download chunks of the three-stage pipeline (pipeline_h2d_d2h),
+                           // 6-7 second input group / output group of a grouped batch (batch_api.cpp)
   hipEvent_t xfer_ev[4] = {};  // chunk buffer 2 + k's copy has finished
   hipStream_t up = nullptr, dn = nullptr;  // pipeline_h2d_d2h: H2D and D2H copy streams
   // zt_timing_enable: HIP-event kernel timing
   bool timing = false;
   hipEvent_t ev[8] = {};  // [2k, 2k+1]: interval k (0 match, 1 deflate pipeline, 2 inflate)
   zt_kernel_times times = {};
-  size_t pinned_size[6] = {};
+  size_t pinned_size[8] = {};
 };
 
 // Records the begin / end event of interval k (0 or 1) when timing is on.
