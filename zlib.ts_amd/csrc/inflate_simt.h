@@ -250,6 +250,69 @@ __device__ __forceinline__ uint32_t from_prev_lane(uint32_t v, uint32_t first) {
   return (uint32_t)__builtin_amdgcn_update_dpp((int)first, (int)v, 0x138, 0xF, 0xF, false);
 }
 
+// ---- phase maps: blocks whose literal / length code is nearly fixed-length
+// (the reference's single block over random bytes: ~8-bit codes) do not
+// resynchronise -- a decode started off a token boundary stays off it, and
+// the repairs above fix one lane per iteration.  For such blocks every lane
+// instead maps each start phase x = 0..14 (bits past s_l) to the phase at
+// which that decode crosses into the next lane's range (15: it ends the
+// block, breaks, or crosses 15 or more bits past it); a prefix composition
+// over the lanes gives every lane's true start at once.
+#ifndef ZT_NO_PHASE_MAPS
+__device__ __forceinline__ bool near_fixed_code(const HuffTab *lt) {
+  // >= 90 % of the code space at one length
+  uint32_t mx = 0;
+#pragma unroll
+  for (int k = 1; k < 16; ++k) {
+    const uint32_t m = lt->count[k] << (15 - k);
+    mx = m > mx ? m : mx;
+  }
+  return mx >= 29491u;
+}
+
+__device__ uint64_t lane_phase_map(LaneBits &lb, uint64_t b0, uint32_t s_l, uint32_t limit, bool in_range,
+                                   const HuffTab *lt, const HuffTab *dt) {
+  uint64_t map = ~0ull;
+  const uint32_t s_next = s_l + SP_LANE_BITS;
+  // a token boundary lies within the longest code past s_l when the token
+  // straddling s_l is a literal (matches are rare in these blocks; a phase
+  // not mapped stays 15 = unknown, and that lane takes the ordinary repair)
+  const uint32_t xmax = lt->maxlen < 15 ? (uint32_t)lt->maxlen : 15u;
+#pragma unroll 1
+  for (uint32_t x = 0; x < xmax; ++x) {
+    bool act = in_range;
+    if (act) lb.init(b0 + s_l + x, s_l + x);
+    uint32_t ph = 15;
+    while (__ballot(act)) {
+      if (act) {
+        uint32_t tk, nb;
+        const int r = lane_token(lb, lt, dt, tk, nb);
+        if (r != 0 || lb.rel > limit) {
+          act = false;
+        } else if (lb.rel >= s_next) {
+          const uint32_t d = lb.rel - s_next;
+          ph = d < 15 ? d : 15;
+          act = false;
+        }
+      }
+    }
+    map = (map & ~(0xFull << (4 * x))) | ((uint64_t)ph << (4 * x));
+  }
+  return map;
+}
+
+// (a o b)[x] = a[b[x]] for 16-entry nibble maps
+__device__ __forceinline__ uint64_t compose_maps(uint64_t a, uint64_t b) {
+  uint64_t r = 0;
+#pragma unroll
+  for (int x = 0; x < 16; ++x) {
+    const uint32_t v = (uint32_t)(b >> (4 * x)) & 15u;
+    r |= ((a >> (4 * v)) & 15ull) << (4 * x);
+  }
+  return r;
+}
+#endif
+
 // Decode the body of a Huffman block that starts at bit `b0` (relative to
 // rd's abase) with the tables in lt / dt.  Tokens go to to.tok[to.ntok ...].
 // Returns 0 with *end_bit = the bit after the end-of-block code, 1 when the
@@ -274,6 +337,9 @@ __device__ int tok_huffman_simt(Reader &rd, uint64_t b0, const HuffTab *lt, cons
   lb.stage = stage;
   uint32_t R = 0;  // true start of this round (bits from b0)
   int dump_round = 0;
+#ifndef ZT_NO_PHASE_MAPS
+  const bool fixedish = near_fixed_code(lt);
+#endif
   for (;;) {
     // ---- stage the round's input: bytes [a0, a0 + SP_STAGE_BYTES)
     const uint64_t a0 = ((b0 + R) >> 3) & ~uint64_t(15);
@@ -381,6 +447,30 @@ __device__ int tok_huffman_simt(Reader &rd, uint64_t b0, const HuffTab *lt, cons
       }
       if (f == 64) break;  // every lane synchronised, the block continues
       if (!__builtin_amdgcn_readlane((int)in_range, f)) return ZT_E_INPUT_BROKEN;  // runs past the input
+#ifndef ZT_NO_PHASE_MAPS
+      if (fixedish && iter == 0 && __popcll(U) >= 4) {
+        // every lane's true start from the composed phase maps; lanes whose
+        // start is unknown (a path ends or breaks before them) wait for the
+        // ordinary repairs, and the block's end is found as usual
+        uint64_t P = lane_phase_map(lb, b0, s_l, limit, in_range, lt, dt);
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)P, d, 64);
+          const uint32_t hi = (uint32_t)__shfl_up((int)(uint32_t)(P >> 32), d, 64);
+          const uint64_t q = ((uint64_t)hi << 32) | lo;
+          if (lane >= d) P = compose_maps(P, q);
+        }
+        const uint32_t plo = (uint32_t)__shfl_up((int)(uint32_t)P, 1, 64);
+        const uint32_t ph = lane == 0 ? 0u : (plo & 15u);  // (map_{l-1} o ... o map_0)[0]
+        const bool known = in_range && ph < 15;
+        const uint32_t tt = (lane == 0 ? R : s_l) + ph;
+        const bool marked = known && ((sp->bm[ph >> 5][lane] >> (ph & 31)) & 1);
+        todo = known && !marked;
+        if (todo) from = tt;
+        repair = true;
+        continue;
+      }
+#endif
       // re-decode every unsynchronised lane from its (current) true start
       // (a lane whose predecessor stopped short of it waits: that predecessor
       // is off the true path and is repaired first)
