@@ -66,7 +66,8 @@ int zt_set_devices(uint64_t mask);
 const char *zt_last_error_message(void);
 /* Library version string. */
 const char *zt_version(void);
-/* Free a buffer returned by the library. */
+/* Free a buffer returned by the library (every output pointer, batch items
+ * included; never free() them directly: batch items share allocations). */
 void zt_free(void *p);
 
 /* ---- checksums (host pointers) ------------------------------------------ */
@@ -158,7 +159,9 @@ int zt_gzip_compress(const uint8_t *in, size_t n, const zt_gzip_opts *opts, uint
  * device: the buffers are packed at 32 KiB boundaries and uploaded once, the
  * batch deflate pipeline and the batched CRC-32 kernels read the same device
  * bytes, and the devices of zt_set_devices share the batch (largest buffers
- * first onto the least loaded device).  out[i] is malloc'd (zt_free).
+ * first onto the least loaded device).  out[i] is library memory: release
+ * each with zt_free (the outputs of one call may share one allocation, which
+ * goes with its last item).
  * Replaces a loop of new GZip(in[i], opts).compress()  src/GZip.ts:96-194. */
 int zt_gzip_compress_batch(const uint8_t *const *in, const size_t *n, size_t count, const zt_gzip_opts *opts,
                            uint8_t **out, size_t *out_len, int *status);

@@ -39,10 +39,11 @@ struct Framing {
   size_t trailer;
 };
 
+// (dst: the item's place in a batch slab, or null for its own allocation)
 int frame_item(const Framing &fr, size_t n_in, const uint8_t *body, size_t blen, uint32_t crc, uint32_t adler,
-               uint8_t **out, size_t *out_len) {
+               uint8_t **out, size_t *out_len, uint8_t *dst = nullptr) {
   const size_t total = fr.prefix.size() + blen + fr.trailer;
-  uint8_t *h = host_out(total);
+  uint8_t *h = dst ? dst : host_out(total);
   if (!h) return set_error(ZT_E_NOMEM, "host allocation failed");
   if (!fr.prefix.empty()) memcpy(h, fr.prefix.data(), fr.prefix.size());
   if (blen) memcpy(h + fr.prefix.size(), body, blen);
@@ -56,6 +57,18 @@ int frame_item(const Framing &fr, size_t n_in, const uint8_t *body, size_t blen,
   *out = h;
   *out_len = total;
   return ZT_OK;
+}
+
+// items [k0, k0 + nb) framed into one slab (slab_out): their offsets, and
+// the slab (null when it cannot be allocated)
+uint8_t *frame_slab(const Framing &fr, const uint64_t *oo, size_t nb, std::vector<size_t> &soff) {
+  soff.resize(nb);
+  size_t tot = 0;
+  for (size_t j = 0; j < nb; ++j) {
+    soff[j] = tot;
+    tot += (fr.prefix.size() + (oo[j + 1] - oo[j]) + fr.trailer + 64) & ~size_t(63);
+  }
+  return slab_out(tot, nb);
 }
 
 // Large shares (>= kGroupMin padded bytes): the items are cut, in order, into
@@ -176,10 +189,13 @@ int batch_grouped(DeviceCtx *c, const uint8_t *const *in, const std::vector<size
       ZT_HIP(hipMemcpyAsync(stage_out, (uint8_t *)d_out + ooff[g], go[nb], hipMemcpyDeviceToHost, c->dn));
       ZT_HIP(hipStreamSynchronize(c->dn));
       std::vector<int> rcs(nb, ZT_OK);
+      std::vector<size_t> soff;
+      uint8_t *slab = frame_slab(fr, go, nb, soff);
+      if (!slab) return set_error(ZT_E_NOMEM, "host allocation failed");
       parallel_copy(nb, [&](size_t j) {
         const size_t k = k0 + j, i = work[k];
         rcs[j] = frame_item(fr, len[k], stage_out + go[j], go[j + 1] - go[j], hsums[2 * k], hsums[2 * k + 1], &out[i],
-                            &out_len[i]);
+                            &out_len[i], slab + soff[j]);
       }, go[nb]);
       for (int rc : rcs)
         if (rc) return rc;
@@ -334,10 +350,13 @@ int batch_on_device(int dev, const uint8_t *const *in, const size_t *n, const st
   ZT_HIP(hipStreamSynchronize(c->aux));
   int first_rc = ZT_OK;
   std::vector<int> rcs(m, ZT_OK);
+  std::vector<size_t> soff;
+  uint8_t *slab = frame_slab(fr, oo.data(), m, soff);
+  if (!slab) return fail(set_error(ZT_E_NOMEM, "host allocation failed"));
   parallel_copy(m, [&](size_t k) {
     const size_t i = work[k];
     rcs[k] = frame_item(fr, len[k], body_host + oo[k], oo[k + 1] - oo[k], hsums[2 * k], hsums[2 * k + 1], &out[i],
-                        &out_len[i]);
+                        &out_len[i], slab + soff[k]);
   }, oo[m]);
   for (int rc : rcs)
     if (rc && !first_rc) first_rc = rc;
@@ -392,7 +411,7 @@ int run_batch(const uint8_t *const *in, const size_t *n, size_t count, int ct, i
   }
   if (first) {
     for (size_t i = 0; i < count; ++i) {
-      free(out[i]);
+      zt_free(out[i]);
       out[i] = nullptr;
       out_len[i] = 0;
     }

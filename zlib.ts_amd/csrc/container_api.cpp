@@ -74,12 +74,12 @@ int deflate_with_checksums(const uint8_t *in, size_t n, const zt_deflate_opts *o
   if (!h) return set_error(ZT_E_NOMEM, "host allocation failed");
   if (prefix_len) memcpy(h, prefix, prefix_len);
   if (const int rc = download(c, h + prefix_len, d_out, len, c->stream)) {
-    free(h);
+    zt_free(h);
     return rc;
   }
   hipError_t e = hipStreamSynchronize(c->aux);
   if (e != hipSuccess) {
-    free(h);
+    zt_free(h);
     return hip_fail(e, "hipStreamSynchronize");
   }
   if (crc) *crc = sums[0];
@@ -247,20 +247,20 @@ int zt_gunzip(const uint8_t *in, size_t n, uint8_t **out, size_t *out_len, zt_gz
     uint32_t crc = 0;
     const int rc = zt_crc32_update(0, o, olen, &crc);
     if (rc) {
-      free(o);
+      zt_free(o);
       return rc;
     }
     Reader t{in, n, eip};
     uint32_t want = 0, isize = 0;
     for (int k = 0; k < 4; ++k) want |= t.u8() << (8 * k);
     if (crc != want) {
-      free(o);
+      zt_free(o);
       snprintf(msg, sizeof msg, "invalid CRC-32 checksum: 0x%x / 0x%x", crc, want);
       return set_error(ZT_E_GZIP_CRC32, msg);
     }
     for (int k = 0; k < 4; ++k) isize |= t.u8() << (8 * k);
     if ((uint32_t)olen != isize) {
-      free(o);
+      zt_free(o);
       snprintf(msg, sizeof msg, "invalid input size: %u / %u", (uint32_t)olen, isize);
       return set_error(ZT_E_GZIP_ISIZE, msg);
     }
@@ -269,7 +269,7 @@ int zt_gunzip(const uint8_t *in, size_t n, uint8_t **out, size_t *out_len, zt_gz
     m.data_off = data.size();
     m.data_len = olen;
     data.insert(data.end(), o, o + olen);
-    free(o);
+    zt_free(o);
     mem.push_back(m);
     ip = t.p;
   }
@@ -281,7 +281,7 @@ int zt_gunzip(const uint8_t *in, size_t n, uint8_t **out, size_t *out_len, zt_gz
   if (members) {
     *members = (zt_gzip_member *)malloc((mem.size() ? mem.size() : 1) * sizeof(zt_gzip_member));
     if (!*members) {
-      free(h);
+      zt_free(h);
       return set_error(ZT_E_NOMEM, "host allocation failed");
     }
     if (!mem.empty()) memcpy(*members, mem.data(), mem.size() * sizeof(zt_gzip_member));
@@ -338,14 +338,14 @@ int zt_zlib_decompress(const uint8_t *in, size_t n, size_t index, int verify, ui
     // src/Inflate.ts:80-90 (the Adler-32 of the output, on the GPU)
     const int rc = zt_adler32_update(1, o, olen, &adler);
     if (rc) {
-      free(o);
+      zt_free(o);
       return rc;
     }
     Reader t{in, n, eip};
     uint32_t want = 0;
     for (int k = 0; k < 4; ++k) want = (want << 8) | t.u8();
     if (adler != want) {
-      free(o);
+      zt_free(o);
       return set_error(ZT_E_ZLIB_ADLER, "invalid adler-32 checksum");
     }
   }

@@ -139,7 +139,7 @@ static int deflate_raw_pipelined(DeviceCtx *c, const uint8_t *in, size_t n, int 
       },
       h, pb * np, &total);
   if (rc) {
-    free(h);
+    zt_free(h);
     return rc;
   }
   *out = h;  // (its pages past the stream were never touched)
@@ -169,7 +169,7 @@ int zt_deflate_raw(const uint8_t *in, size_t n, const zt_deflate_opts *opts, uin
   if (!h) return set_error(ZT_E_NOMEM, "host allocation failed");
   const int rc = download(c, h, d_out, len, c->stream);
   if (rc) {
-    free(h);
+    zt_free(h);
     return rc;
   }
   *out = h;

@@ -1,6 +1,7 @@
 // inflate_api.cpp -- host side of the inflate entry points (include/zt.h).
 #include <algorithm>
 #include <cstdio>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -39,6 +40,17 @@ static size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 // Streams it cannot finish (errors, a token overflow, an empty input) are
 // appended to `failed` for the one-wave decoder, which also yields the
 // reference's exact error. Outputs of the others are malloc'd and filled.
+// ZT_BATCH_TIMING=1: host wall time of the batch stages on stderr (measurement only)
+static double bt_now() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+static bool bt_on() {
+  static const bool on = getenv("ZT_BATCH_TIMING") != nullptr;
+  return on;
+}
+#define BT(label) \
+  if (bt_on()) fprintf(stderr, "[batch] %-28s %8.2f ms\n", label, bt_now())
+
 static int batch_two_phase(DeviceCtx *c, const uint8_t *d_in, const std::vector<size_t> &in_off, const size_t *n,
                            const size_t *index, size_t count, uint8_t **out, size_t *out_len,
                            std::vector<InfResult> &res, std::vector<size_t> &failed) {
@@ -89,10 +101,12 @@ static int batch_two_phase(DeviceCtx *c, const uint8_t *d_in, const std::vector<
   tp.dbg = nullptr;
   tp.dump_unit = 0xFFFFFFFFu;
   tp.dump_once = 0;
+  BT("tokenize launch");
   ZT_TRY(tokenize_units_dev(tp, s));
   std::vector<TokResult> tr(units);
   ZT_HIP(hipMemcpyAsync(tr.data(), d_tres, units * sizeof(TokResult), hipMemcpyDeviceToHost, s));
   ZT_HIP(hipStreamSynchronize(s));
+  BT("tokenize done");
   // one chain unit and one segment per stream that decoded to BFINAL
   std::vector<ChainUnit> chain;
   std::vector<SegJob> segs;
@@ -144,16 +158,28 @@ static int batch_two_phase(DeviceCtx *c, const uint8_t *d_in, const std::vector<
   ZT_TRY(pinned(c, out_total, &h));
   ZT_HIP(hipMemcpyAsync(h, d_out, out_total, hipMemcpyDeviceToHost, s));
   ZT_HIP(hipStreamSynchronize(s));
+  BT("resolve + D2H done");
   const uint8_t *stage = static_cast<const uint8_t *>(h);
   std::vector<size_t> done;
+  for (size_t j = 0; j < chain.size(); ++j)
+    if (ust[j] == ZT_OK && sst[j] == ZT_OK) done.push_back(j);
+  // the finished outputs share one slab (slab_out), 64-byte aligned items
+  size_t slab_total = 0;
+  std::vector<size_t> soff(done.size());
+  for (size_t q = 0; q < done.size(); ++q) {
+    soff[q] = slab_total;
+    slab_total += align_up(chain[done[q]].out_len ? chain[done[q]].out_len : 1, 64);
+  }
+  uint8_t *slab = done.empty() ? nullptr : slab_out(slab_total, done.size());
+  if (!done.empty() && !slab) return set_error(ZT_E_NOMEM, "host allocation failed");
+  size_t dq = 0;
   for (size_t j = 0; j < chain.size(); ++j) {
     const size_t k = who[j], i = ids[k];
     if (ust[j] != ZT_OK || sst[j] != ZT_OK) {
       failed.push_back(i);
       continue;
     }
-    out[i] = (uint8_t *)malloc(chain[j].out_len ? chain[j].out_len : 1);
-    if (!out[i]) return set_error(ZT_E_NOMEM, "host allocation failed");
+    out[i] = slab + soff[dq++];
     out_len[i] = chain[j].out_len;
     InfResult &r = res[i];
     r = InfResult{};
@@ -161,12 +187,13 @@ static int batch_two_phase(DeviceCtx *c, const uint8_t *d_in, const std::vector<
     r.end_ip = ((tr[k].end_bits + 7) >> 3) - in_off[i];
     r.status = ZT_OK;
     r.stop_idx = -1;
-    done.push_back(j);
   }
+  BT("mallocs done");
   parallel_copy(done.size(), [&](size_t q) {
     const size_t j = done[q], i = ids[who[j]];
     if (chain[j].out_len) memcpy(out[i], stage + chain[j].out_off, chain[j].out_len);
   }, out_total);
+  BT("copies done");
   return ZT_OK;
 }
 
@@ -297,7 +324,9 @@ static int inflate_host_batch(const uint8_t *const *in, const size_t *n, const s
     void *h;
     ZT_TRY(pinned(c, in_total, &h));
     uint8_t *stage = (uint8_t *)h;
+    BT("pack start");
     parallel_copy(count, [&](size_t i) { if (n[i]) memcpy(stage + in_off[i], in[i], n[i]); }, in_total);
+    BT("pack done");
     ZT_HIP(hipMemcpyAsync(d_in, stage, in_total, hipMemcpyHostToDevice, c->stream));
   }
   return inflate_dev_batch(c, d_in, in_off, n, index, count, strict, out, out_len, end_ip, status);
@@ -323,7 +352,7 @@ int inflate_dev_member(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t index
         if (!h) return set_error(ZT_E_NOMEM, "host allocation failed");
         const int rc = download(c, h, d_out, ol, s);
         if (rc) {
-          free(h);
+          zt_free(h);
           return rc;
         }
         *out = h;
@@ -367,7 +396,7 @@ int zt_inflate_raw(const uint8_t *in, size_t n, size_t index, const zt_inflate_o
       if (!h) return set_error(ZT_E_NOMEM, "host allocation failed");
       const int rc = download(c, h, d_out, ol, c->stream);
       if (rc) {
-        free(h);
+        zt_free(h);
         return rc;
       }
       *out = h;
@@ -449,7 +478,7 @@ int zt_inflate_raw_resume(const uint8_t *in, size_t n, uint64_t bit_pos, const u
     if (!h) return set_error(ZT_E_NOMEM, "host allocation failed");
     const int rc = download(c, h, d_out, done, c->stream);
     if (rc) {
-      free(h);
+      zt_free(h);
       return rc;
     }
     *out = h;

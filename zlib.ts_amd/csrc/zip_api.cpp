@@ -71,7 +71,7 @@ int zt_zip_compress(const uint8_t *const *in, const size_t *n, const zt_zip_file
   struct Freer {
     std::vector<uint8_t *> &v;
     ~Freer() {
-      for (uint8_t *p : v) free(p);
+      for (uint8_t *p : v) zt_free(p);
     }
   } freer{body};
   std::vector<size_t> defl, stored;
@@ -272,7 +272,7 @@ int zt_unzip(const uint8_t *in, size_t n, int verify, uint8_t **out, size_t *out
   struct Freer {
     std::vector<uint8_t *> &v;
     ~Freer() {
-      for (uint8_t *p : v) free(p);
+      for (uint8_t *p : v) zt_free(p);
     }
   } freer{o};
   if (!defl.empty()) {
@@ -301,7 +301,7 @@ int zt_unzip(const uint8_t *in, size_t n, int verify, uint8_t **out, size_t *out
         ent[i].status = st[k];
         inflate_error(st[k], 0);
         snprintf(ent[i].message, sizeof ent[i].message, "%s", zt_last_error_message());
-        free(bp[k]);
+        zt_free(bp[k]);
         continue;
       }
       o[i] = bp[k];
@@ -338,7 +338,7 @@ int zt_unzip(const uint8_t *in, size_t n, int verify, uint8_t **out, size_t *out
   if (total) {
     const int rc = zt_crc32_batch(cp.data(), cn.data(), total, dcrc.data());
     if (rc) {
-      free(h);
+      zt_free(h);
       return rc;
     }
   }
@@ -352,7 +352,7 @@ int zt_unzip(const uint8_t *in, size_t n, int verify, uint8_t **out, size_t *out
   }
   zt_unzip_entry *E = (zt_unzip_entry *)malloc((total ? total : 1) * sizeof(zt_unzip_entry));
   if (!E) {
-    free(h);
+    zt_free(h);
     return set_error(ZT_E_NOMEM, "host allocation failed");
   }
   if (total) memcpy(E, ent.data(), total * sizeof(zt_unzip_entry));

@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <condition_variable>
 #include <functional>
+#include <map>
 #include <thread>
 #include <cstdio>
 #include <cstdlib>
@@ -118,6 +119,40 @@ uint8_t *host_out(size_t n) {
   if (posix_memalign(&p, 2u << 20, n)) return nullptr;
   (void)madvise(p, n, MADV_HUGEPAGE);
   return (uint8_t *)p;
+}
+
+// Batch outputs share one host allocation (a slab, on huge pages when large):
+// one allocation and one stream of first-touch faults instead of one per
+// item (4096 x 64 KiB outputs: 21 ms of faults in the copy-out).  Each item
+// pointer is still released by zt_free; the slab goes with its last item.
+struct Slab {
+  size_t size;
+  size_t refs;
+};
+static std::mutex g_slab_mu;
+static std::map<uintptr_t, Slab> g_slabs;
+
+uint8_t *slab_out(size_t total, size_t items) {
+  if (total == 0) total = 1;
+  uint8_t *b = host_out(total);
+  if (!b) return nullptr;
+  std::lock_guard<std::mutex> lk(g_slab_mu);
+  g_slabs[(uintptr_t)b] = Slab{total, items};
+  return b;
+}
+
+bool slab_release(void *p) {
+  std::lock_guard<std::mutex> lk(g_slab_mu);
+  if (g_slabs.empty()) return false;
+  auto it = g_slabs.upper_bound((uintptr_t)p);
+  if (it == g_slabs.begin()) return false;
+  --it;
+  if ((uintptr_t)p >= it->first + it->second.size) return false;
+  if (--it->second.refs == 0) {
+    free(reinterpret_cast<void *>(it->first));
+    g_slabs.erase(it);
+  }
+  return true;
 }
 
 int pinned(DeviceCtx *c, size_t bytes, void **ptr, int slot) {
@@ -415,7 +450,11 @@ const char *zt_last_error_message(void) { return g_err.c_str(); }
 
 const char *zt_version(void) { return "zlib.ts_amd 0.1 (gfx950)"; }
 
-void zt_free(void *p) { free(p); }
+void zt_free(void *p) {
+  if (!p) return;
+  if (slab_release(p)) return;
+  free(p);
+}
 
 int zt_dev_checksums(const void *d_in, size_t n, uint32_t crc_in, uint32_t adler_in, uint32_t *crc_out,
                      uint32_t *adler_out, void *stream) {

@@ -76,6 +76,11 @@ int scratch(DeviceCtx *c, int slot, size_t bytes, void **ptr);
 int pinned(DeviceCtx *c, size_t bytes, void **ptr, int slot = 0);
 // Host output buffer the caller frees with zt_free (large ones on huge pages).
 uint8_t *host_out(size_t n);
+// One host allocation for `items` batch outputs (pointers inside it, each
+// released by zt_free; reserve >= 1 byte per item so every pointer is
+// distinct).  slab_release: true when p lay in a slab (and was released).
+uint8_t *slab_out(size_t total, size_t items);
+bool slab_release(void *p);
 // fn(0 .. count-1) over a few host threads when total_bytes is large.
 void parallel_copy(size_t count, const std::function<void(size_t)> &fn, size_t total_bytes);
 
