@@ -322,6 +322,10 @@ __device__ __forceinline__ uint64_t compose_maps(uint64_t a, uint64_t b) {
 // not decoded).  bm_out (global, SP_WORDS * 64 words): the token-start bitmap
 // of the path's first round (bit x = a token starts at b0 + x), for the
 // speculative tokenizer's sync test.
+// PHASE: phase maps for near-fixed-length codes (the sync-point / batch
+// tokenizer; the general tokenizer keeps them off: their registers cost it a
+// wave per SIMD, 3 -> 2, and its units start mid-block anyway)
+template <bool PHASE = false>
 __device__ int tok_huffman_simt(Reader &rd, uint64_t b0, const HuffTab *lt, const HuffTab *dt, TokOut &to,
                                 uint64_t &op, SpecShared *sp, uint64_t &end_bit, uint32_t *dump = nullptr,
                                 uint32_t stop_rel = 0xFFFFFFFFu, uint32_t *bm_out = nullptr,
@@ -338,7 +342,7 @@ __device__ int tok_huffman_simt(Reader &rd, uint64_t b0, const HuffTab *lt, cons
   uint32_t R = 0;  // true start of this round (bits from b0)
   int dump_round = 0;
 #ifndef ZT_NO_PHASE_MAPS
-  const bool fixedish = near_fixed_code(lt);
+  const bool fixedish = PHASE && near_fixed_code(lt);
 #endif
   for (;;) {
     // ---- stage the round's input: bytes [a0, a0 + SP_STAGE_BYTES)
@@ -448,7 +452,9 @@ __device__ int tok_huffman_simt(Reader &rd, uint64_t b0, const HuffTab *lt, cons
       if (f == 64) break;  // every lane synchronised, the block continues
       if (!__builtin_amdgcn_readlane((int)in_range, f)) return ZT_E_INPUT_BROKEN;  // runs past the input
 #ifndef ZT_NO_PHASE_MAPS
-      if (fixedish && iter == 0 && __popcll(U) >= 4) {
+      // (text regions of such a block repair a few lanes cheaply: maps only
+      // when many lanes missed)
+      if (PHASE && fixedish && iter == 0 && __popcll(U) >= 8) {
         // every lane's true start from the composed phase maps; lanes whose
         // start is unknown (a path ends or breaks before them) wait for the
         // ordinary repairs, and the block's end is found as usual

@@ -103,7 +103,7 @@ __global__ __launch_bounds__(64) void tokenize_kernel(TokParams P) {
       const uint32_t nt_before = uni(to.ntok);
       const uint64_t op_before = op;
       uint32_t *dump = (P.dbg && u == P.dump_unit && P.dump_once == 0) ? reinterpret_cast<uint32_t *>(P.dbg + (uint64_t)P.count * 8) : nullptr;
-      int r = P.simt ? tok_huffman_simt(rd, body0, &sh.lit, &sh.dist, to, op, &spsh, end_bit, dump) : 1;
+      int r = P.simt ? tok_huffman_simt<true>(rd, body0, &sh.lit, &sh.dist, to, op, &spsh, end_bit, dump) : 1;
       if (P.dbg && r == 0) {
         // shadow check: decode the same body with one lane and compare
         const uint64_t s_end = end_bit, s_op = op;
