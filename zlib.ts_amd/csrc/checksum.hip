@@ -15,8 +15,9 @@
 //     multiplication (earlier design: one contiguous 1 KiB slice per lane,
 //     64 cache lines per load instruction and no L1 reuse, 23 % of HBM);
 //   * CRC lookups: nibble tables, each replicated 32x in LDS so that lane l
-//     always reads bank l -- every ds_read_b32 is conflict-free (2.5
-//     lookups/byte);  Adler: v_dot4_u32_u8 sums per piece, positions weighted
+//     always reads bank l -- every ds_read_b32 is conflict-free (2.25
+//     lookups/byte); one v_perm_b32 per lookup address, 3-input XORs
+//     (v_bitop3_b32);  Adler: v_dot4_u32_u8 sums per piece, positions weighted
 //     from the piece's place in the segment;
 //   * per-lane results are merged with polynomial shifts (CRC) and weighted
 //     sums (Adler) inside the workgroup, then one tiny kernel merges segments.
@@ -72,27 +73,53 @@ __device__ __forceinline__ uint4 ld_stream(const uint4 *p) {
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
-__device__ __forceinline__ uint32_t lut(const uint32_t *T, int pos, uint32_t nib, int lane) {
-  return T[(((pos << 4) + nib) << 5) + lane];
+// Nibble table layout in LDS (byte address): position pos (0..23), nibble
+// value v, replica r = lane & 31 at (pos >> 1) * 4096 + v * 256 + (pos & 1) *
+// 128 + 4 r.  Lane l always reads bank l & 31 (conflict-free), and a lookup's
+// address is one v_perm_b32: byte 0 the lane's 4 r, byte 1 the nibble, taken
+// from a word whose bytes hold nibbles (a & 0x0F0F0F0F or (a >> 4) & ...);
+// the table position is the ds_read's immediate offset.
+__device__ __forceinline__ uint32_t nib_index(uint32_t i) {  // LDS word i -> nib_g entry
+  const uint32_t pos = ((i >> 10) << 1) | ((i >> 5) & 1u);
+  return (pos << 4) + ((i >> 6) & 15u);
+}
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+// the 8 lookups of word a's nibbles in tables P0 .. P0 + 7 (P0 even)
+template <int P0>
+__device__ __forceinline__ void lut8(uint32_t a, const uint32_t *T, uint32_t lb, uint32_t *t) {
+  const uint32_t me = a & 0x0F0F0F0Fu, mo = (a >> 4) & 0x0F0F0F0Fu;
+  const char *Tb = reinterpret_cast<const char *>(T);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t sel = 0x0C0C0400u | ((uint32_t)k << 8);
+    const uint32_t ae = __builtin_amdgcn_perm(me, lb, sel), ao = __builtin_amdgcn_perm(mo, lb, sel);
+    t[2 * k] = *reinterpret_cast<const uint32_t *>(Tb + ae + (P0 / 2 + k) * 4096);
+    t[2 * k + 1] = *reinterpret_cast<const uint32_t *>(Tb + ao + (P0 / 2 + k) * 4096 + 128);
+  }
 }
 
 // One 8-byte CRC step: state xors into the first 4 bytes (reflected slice-by-8).
-__device__ __forceinline__ uint32_t crc_step8(uint32_t c, uint32_t w0, uint32_t w1, const uint32_t *T, int lane) {
-  uint32_t a = c ^ w0;
-  uint32_t r = 0;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r ^= lut(T, j, (a >> (4 * j)) & 15u, lane);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r ^= lut(T, 8 + j, (w1 >> (4 * j)) & 15u, lane);
-  return r;
+// lb = 4 * (lane & 31)
+__device__ __forceinline__ uint32_t crc_step8(uint32_t c, uint32_t w0, uint32_t w1, const uint32_t *T, uint32_t lb) {
+  uint32_t t[16];
+  lut8<8>(w1, T, lb, t + 8);
+  lut8<0>(c ^ w0, T, lb, t);
+  const uint32_t x0 = xor3(t[8], t[9], t[10]), x1 = xor3(t[11], t[12], t[13]), x2 = xor3(t[14], t[15], t[0]);
+  const uint32_t x3 = xor3(t[1], t[2], t[3]), x4 = xor3(t[4], t[5], t[6]);
+  return xor3(x0, x1, x2) ^ xor3(x3, x4, t[7]);
 }
 
-// c * x^(8 * CK_RB) mod P (the lane stream's advance by one row)
-__device__ __forceinline__ uint32_t crc_adv1k(uint32_t c, const uint32_t *T, int lane) {
-  uint32_t r = 0;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r ^= lut(T, ADV + j, (c >> (4 * j)) & 15u, lane);
-  return r;
+// c * x^(8 * CK_RB) mod P (the lane stream's advance by one row), xor x
+__device__ __forceinline__ uint32_t crc_adv1k(uint32_t c, uint32_t x, const uint32_t *T, uint32_t lb) {
+  uint32_t t[8];
+  lut8<ADV>(c, T, lb, t);
+  return xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), xor3(t[6], t[7], x));
 }
 
 __device__ __forceinline__ uint32_t crc_byte(uint32_t c, uint32_t b) {
@@ -146,13 +173,13 @@ __global__ __launch_bounds__(CK_THREADS) void checksum_segments(const uint8_t *_
   __shared__ uint32_t red_w[CK_THREADS / 64];
 
   const int tid = threadIdx.x;
-  const int lane32 = tid & 31;
+  const uint32_t lane32 = 4u * (uint32_t)(tid & 31);  // the lane's replica byte offset
   if (DO_CRC) {
     // all loads in flight before the LDS stores (one call's latency matters
     // for small inputs)
     uint32_t tv[NIB_ENTRIES * 32 / CK_THREADS];
 #pragma unroll
-    for (int k = 0; k < NIB_ENTRIES * 32 / CK_THREADS; ++k) tv[k] = nib_g[(tid + k * CK_THREADS) >> 5];
+    for (int k = 0; k < NIB_ENTRIES * 32 / CK_THREADS; ++k) tv[k] = nib_g[nib_index(tid + k * CK_THREADS)];
 #pragma unroll
     for (int k = 0; k < NIB_ENTRIES * 32 / CK_THREADS; ++k) T[tid + k * CK_THREADS] = tv[k];
     if (tid < 32) x2n[tid] = x2n_g[tid];
@@ -209,7 +236,7 @@ __global__ __launch_bounds__(CK_THREADS) void checksum_segments(const uint8_t *_
               const uint4 x = v[k * CK_Q + j];
               r = crc_step8(crc_step8(r, x.x, x.y, T, lane32), x.z, x.w, T, lane32);
             }
-            L = crc_adv1k(L, T, lane32) ^ r;
+            L = crc_adv1k(L, r, T, lane32);
           }
           if (DO_ADLER) {
 #pragma unroll
