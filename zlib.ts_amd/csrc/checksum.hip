@@ -7,10 +7,11 @@
 //     0.63 ms, 256 threads with 4 / 8 / 16 rows per batch 0.44 / 0.41-0.43
 //     / 0.49 ms per GiB);
 //   * loads are coalesced: each wave instruction reads 1 KiB contiguous, lane l
-//     the 16 bytes at 16 l, so lane l's bytes are 16-byte pieces 1 KiB apart.
-//     Its CRC is kept as a lane stream: L <- L * x^(8 * 1024) + raw(piece)
-//     (raw: the piece's CRC from state 0, slice-by-8 twice; the multiplication
-//     by the constant: 8 lookups in nibble tables of x^(8 * 1024) * v), and
+//     the 16 bytes at 16 l; a row is CK_Q such loads, so lane l's bytes are
+//     CK_P = 16 CK_Q-byte pieces CK_RB = 64 CK_P bytes apart.
+//     Its CRC is kept as a lane stream: L <- L * x^(8 * CK_RB) + raw(piece)
+//     (raw: the piece's CRC from state 0, slice-by-8 steps; the multiplication
+//     by the constant: 8 lookups in nibble tables of x^(8 * CK_RB) * v), and
 //     each lane stream is moved to the segment end once, by one
 //     multiplication (earlier design: one contiguous 1 KiB slice per lane,
 //     64 cache lines per load instruction and no L1 reuse, 23 % of HBM);
