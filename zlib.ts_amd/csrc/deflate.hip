@@ -679,7 +679,10 @@ struct HufScratch {
 
 // parse staging ring (parse_block_dma)
 constexpr int PB_CH = 4;
-constexpr int PB_NCH = 5;
+#ifndef ZT_PB_NCH
+#define ZT_PB_NCH 5
+#endif
+constexpr int PB_NCH = ZT_PB_NCH;
 constexpr int PB_LOADS = PB_CH + PB_CH / 4;  // global_load_lds per chunk (res words, then data words)
 struct ParseStage {
   uint32_t res[PB_NCH][PB_CH * 64];
@@ -691,7 +694,6 @@ struct BlockShared {
   uint32_t dist_hist[32];
   uint32_t n_cl_syms, hlit, hdist, hclen;
   union {
-    ParseStage stage;  // the parse's staging ring, then the code construction
     struct {
       uint32_t lit_code[288];
       uint32_t dist_code[32];
@@ -1350,6 +1352,32 @@ __global__ __launch_bounds__(64) void optparse_kernel(DeflateParams P) {
   }
 }
 
+// parse of one block per wave (the DP's path, or the greedy / lazy parse):
+// tokens written over res, literal / length and distance histograms and the
+// token count handed to block_kernel through the start of the block's slot
+// (its prices are consumed by then; block_kernel writes the header there only
+// after reading them).  A kernel of its own so that its LDS (histograms + the
+// LDS-DMA staging ring, 7.5 KiB) keeps 20 waves per CU on this latency-bound
+// walk, instead of block_kernel's 15 (its Huffman scratch, 10.3 KiB).
+__global__ __launch_bounds__(64) void parse_kernel(DeflateParams P) {
+  __shared__ PriceShared sh;
+  PriceShared *s = &sh;
+  const int lane = threadIdx.x;
+  const uint32_t blk = blockIdx.x;
+  const uint64_t lo = (uint64_t)blk * DF_BLOCK;
+  const uint64_t n = stream_end(P, blk);
+  const uint32_t blen = (uint32_t)((n - lo) < DF_BLOCK ? (n - lo) : DF_BLOCK);
+  for (int i = lane; i < 288; i += 64) s->lit_hist[i] = 0;
+  if (lane < 32) s->dist_hist[lane] = 0;
+  wsync();
+  const uint32_t ntok = parse_block<true>(s, &s->stage, P, P.res + lo, P.base + P.halo + lo, blen);
+  wsync();
+  uint32_t *hs = reinterpret_cast<uint32_t *>(P.slots + (size_t)blk * DF_SLOT);
+  for (int i = lane; i < 288; i += 64) hs[i] = s->lit_hist[i];
+  if (lane < 32) hs[288 + lane] = s->dist_hist[lane];
+  if (lane == 0) hs[320] = ntok;
+}
+
 __global__ __launch_bounds__(64) void block_kernel(DeflateParams P) {
   __shared__ BlockShared sh;
   BlockShared *s = &sh;
@@ -1358,12 +1386,13 @@ __global__ __launch_bounds__(64) void block_kernel(DeflateParams P) {
   const uint64_t lo = (uint64_t)blk * DF_BLOCK;
   const uint64_t n = stream_end(P, blk);
   const uint32_t blen = (uint32_t)((n - lo) < DF_BLOCK ? (n - lo) : DF_BLOCK);
-  const uint8_t *data = P.base + P.halo + lo;
-  uint32_t *r_blk = P.res + lo;
   BlockPlan *plan = P.plans + blk;
   const bool last = P.span ? lo + DF_BLOCK >= n : P.final_ && (blk == P.nblocks - 1);
-  for (int i = lane; i < 288; i += 64) s->lit_hist[i] = 0;
-  if (lane < 32) s->dist_hist[lane] = 0;
+  // the parse's histograms and token count (parse_kernel, in the block's slot)
+  const uint32_t *hs = reinterpret_cast<const uint32_t *>(P.slots + (size_t)blk * DF_SLOT);
+  for (int i = lane; i < 288; i += 64) s->lit_hist[i] = hs[i];
+  if (lane < 32) s->dist_hist[lane] = hs[288 + lane];
+  const uint32_t ntok = hs[320];
   wsync();
 #ifdef ZT_DF_TIME
   uint64_t bt0 = __builtin_readcyclecounter(), btk;
@@ -1374,7 +1403,6 @@ __global__ __launch_bounds__(64) void block_kernel(DeflateParams P) {
 #else
 #define BK_T(k) (void)0
 #endif
-  const uint32_t ntok = parse_block<true>(s, &s->stage, P, r_blk, data, blen);
   BK_T(0);
   wsync();
   if (lane == 0) s->lit_hist[256] += 1;  // end of block
@@ -2046,6 +2074,8 @@ int deflate_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t halo, in
     optparse_kernel<<<G.nblocks, 64, 0, s>>>(P);
     ZT_HIP(hipGetLastError());
   }
+  parse_kernel<<<G.nblocks, 64, 0, s>>>(P);
+  ZT_HIP(hipGetLastError());
   block_kernel<<<G.nblocks, 64, 0, s>>>(P);
   ZT_HIP(hipGetLastError());
   encode_kernel<<<G.nblocks, ENC_THREADS, 0, s>>>(P);
@@ -2138,6 +2168,8 @@ int deflate_batch_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t count, const
     optparse_kernel<<<G.nblocks, 64, 0, s>>>(P);
     ZT_HIP(hipGetLastError());
   }
+  parse_kernel<<<G.nblocks, 64, 0, s>>>(P);
+  ZT_HIP(hipGetLastError());
   block_kernel<<<G.nblocks, 64, 0, s>>>(P);
   ZT_HIP(hipGetLastError());
   encode_kernel<<<G.nblocks, ENC_THREADS, 0, s>>>(P);
