@@ -680,7 +680,7 @@ struct HufScratch {
 // parse staging ring (parse_block_dma)
 constexpr int PB_CH = 4;
 #ifndef ZT_PB_NCH
-#define ZT_PB_NCH 5
+#define ZT_PB_NCH 4
 #endif
 constexpr int PB_NCH = ZT_PB_NCH;
 constexpr int PB_LOADS = PB_CH + PB_CH / 4;  // global_load_lds per chunk (res words, then data words)
@@ -930,6 +930,9 @@ __device__ __forceinline__ void lds_inc(uint32_t *p) {
   __asm__ volatile("ds_add_u32 %0, %1" ::"v"(a), "v"(1u) : "memory");
 }
 
+#ifndef ZT_PW_SCALAR
+#define ZT_PW_SCALAR 3  // match lanes up to which a window's path is walked by scalar jumps
+#endif
 // parse -> tokens over res, histograms.  One 64-position window per step:
 // the path through it from `entry` (a scalar walk over the match lanes, or
 // pointer doubling when they are many), its tokens written in order.
@@ -955,7 +958,7 @@ __device__ __forceinline__ void parse_window(S *s, const DeflateParams &P, uint3
     const uint64_t mm = __ballot(i < len && L >= 3);
     uint64_t path = 0;
     uint32_t exit;
-    if (__popcll(mm & (~0ull << entry)) <= 3) {
+    if (__popcll(mm & (~0ull << entry)) <= ZT_PW_SCALAR) {
       uint32_t cur = entry;
       while (cur < 64) {
         const uint64_t rest = mm & (~0ull << cur);
