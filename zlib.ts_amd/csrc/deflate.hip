@@ -1138,15 +1138,20 @@ constexpr int OP_SEG = DF_BLOCK / 64;  // one segment per lane
 constexpr int OP_OV = 128;
 // C ring rows: C[i + l] for l <= OP_RING.  A longer match reads C[i + OP_RING]
 // instead of C[i + L] (an estimate of its continuation: the parse stays
-// valid, only the DP's cost model is approximate there); 80 rows keep the
-// LDS at 11 KiB per wave (12 waves per CU, the VGPR limit, instead of 4 at
-// 260 rows); ratios unchanged to 4 digits on the bench corpora
+// valid, only the DP's cost model is approximate there); 64 rows and 3
+// prefetched groups keep the LDS at 8.5 KiB and the VGPRs at 126 per wave (4
+// waves per SIMD; 80 rows / 4 groups: 3, 2.83 -> 2.73 ms per GiB,
+// profiles/r02q_optparse_variants.txt); bench ratio unchanged to 5 digits
+// (260 rows: 1 wave per SIMD)
 #ifndef ZT_OP_RING
-#define ZT_OP_RING 80
+#define ZT_OP_RING 64
 #endif
 constexpr int OP_RING = ZT_OP_RING;
 constexpr int OP_SHORT = 16;
-constexpr int OP_PF = 4;      // groups of 16 positions prefetched per lane  // every cut length 3..OP_SHORT is tried, longer ones only at L
+#ifndef ZT_OP_PF
+#define ZT_OP_PF 3
+#endif
+constexpr int OP_PF = ZT_OP_PF;      // groups of 16 positions prefetched per lane  // every cut length 3..OP_SHORT is tried, longer ones only at L
 
 // prices of one block, in 1/8 bits (price_kernel -> optparse_kernel), kept at
 // the start of the block's slot until block_kernel writes its header there
