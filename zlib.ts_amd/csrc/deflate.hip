@@ -22,11 +22,12 @@
 //      prices from the greedy parse of the block's first quarter, then a
 //      backward shortest-path DP over every position (cut lengths 3..16 and
 //      the full match), choices written over res.
-//   3. block_kernel -- one wave per block: parse of the DP's choices
-//      (LDS-DMA staged, pointer doubling), histograms, length-limited
-//      Huffman lengths by wave-parallel package-merge, canonical codes, the
-//      RLE'd code-length header, and the smallest of stored / fixed /
-//      dynamic.
+//   3. parse_kernel -- one wave per block: parse of the DP's choices
+//      (LDS-DMA staged, pointer doubling), tokens over res, histograms (a
+//      small LDS footprint: many waves per CU).
+//      block_kernel -- one wave per block: length-limited Huffman lengths by
+//      wave-parallel package-merge, canonical codes, the RLE'd code-length
+//      header, and the smallest of stored / fixed / dynamic.
 //   4. encode_kernel -- 256 threads per block: prefix sum of per-thread bit
 //      counts, word-parallel packing; every block ends byte-aligned with an
 //      empty stored block (00 00 FF FF) so blocks concatenate bytewise.
