@@ -28,7 +28,7 @@
 //      block_kernel -- one wave per block: length-limited Huffman lengths by
 //      wave-parallel package-merge, canonical codes, the RLE'd code-length
 //      header, and the smallest of stored / fixed / dynamic.
-//   4. encode_kernel -- 256 threads per block: prefix sum of per-thread bit
+//   4. encode_kernel -- 512 threads per block: prefix sum of per-thread bit
 //      counts, word-parallel packing; every block ends byte-aligned with an
 //      empty stored block (00 00 FF FF) so blocks concatenate bytewise.
 //   5. scan_sizes + gather_blocks -- exclusive scan of block sizes and a
@@ -81,7 +81,10 @@ constexpr int DF_THREADS = 1024;
 // a super-chunk loads DF_HIST bytes of history first (whole sub-chunks)
 constexpr int DF_HIST = DF_RING - DF_SUB;     // 28672
 constexpr int DF_MAXDIST = DF_HIST - 64;      // 28608
-constexpr int ENC_THREADS = 256;
+#ifndef ZT_ENC_THREADS
+#define ZT_ENC_THREADS 512  // 128 / 256 / 512 / 1024: 1.70 / 1.42 / 1.38 / 1.75 ms per GiB (profiles/r02q_encode_variants.txt)
+#endif
+constexpr int ENC_THREADS = ZT_ENC_THREADS;
 // Independent segments of 1 MiB: restart points for segment-parallel inflate
 constexpr uint32_t kRestartBlocks = (1u << 20) / DF_BLOCK;  // 1 MiB
 // empty head entry: p - kNoHead exceeds DF_MAXDIST for every rel position p
