@@ -39,7 +39,12 @@ struct TokShared {
 };
 
 
-__global__ __launch_bounds__(64) void tokenize_kernel(TokParams P) {
+#ifdef ZT_TOK_WAVES
+#define ZT_TOK_ATTR __attribute__((amdgpu_waves_per_eu(ZT_TOK_WAVES)))
+#else
+#define ZT_TOK_ATTR
+#endif
+__global__ __launch_bounds__(64) ZT_TOK_ATTR void tokenize_kernel(TokParams P) {
   __shared__ TokShared sh;
   __shared__ SpecShared spsh;
   const uint32_t u = blockIdx.x;
