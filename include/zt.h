@@ -125,6 +125,13 @@ int zt_inflate_raw(const uint8_t *in, size_t n, size_t index, const zt_inflate_o
  * output is identical. */
 int zt_inflate_raw_resume(const uint8_t *in, size_t n, uint64_t bit_pos, const uint8_t *window, size_t wlen,
                           uint8_t **out, size_t *out_len, uint64_t *end_bits, int *finished);
+/* The same for the last piece of a stream (no more input will come): every
+ * error is reported as-is -- a stream that is corrupt near its end, or ends
+ * before its BFINAL block, fails with the reference's message instead of
+ * waiting for more input (RawInflateStream.finish() in the JS / Python
+ * facades). */
+int zt_inflate_raw_resume_final(const uint8_t *in, size_t n, uint64_t bit_pos, const uint8_t *window, size_t wlen,
+                                uint8_t **out, size_t *out_len, uint64_t *end_bits, int *finished);
 
 /* Batch forms: `count` independent buffers in one launch (config C2/C4).
  * status[i] receives each item's code; the call returns the first failure. */

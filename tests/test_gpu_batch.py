@@ -143,3 +143,26 @@ def test_grouped_batch_equals_single_pipeline(zt, kind):
     for f, mb in zip(files[::97], whole[::97]):
         dec = zlib.decompress(mb, 31 if kind == "gzip" else 15)
         assert dec == f
+
+
+@pytest.mark.parametrize("ndev", [2, 3])
+def test_alias_devices_split(ndev):
+    """The multi-device batch split (zt_set_devices: LPT over the devices, one
+    host thread and one context per device, batch_api.cpp run_batch) run on
+    this one GPU: ZT_ALIAS_DEVICES makes the library present `ndev` logical
+    devices, each with its own context.  Every member spread over them equals
+    the one-device member and decodes with the oracle (tests/alias_batch_child.py,
+    a child process: the alias is read once when the library loads)."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, ZT_ALIAS_DEVICES=str(ndev))
+    p = subprocess.run([sys.executable, os.path.join(here, "alias_batch_child.py"), str(ndev)], env=env,
+                       capture_output=True, text=True, timeout=100)
+    assert p.returncode == 0, p.stderr[-2000:]
+    res = json.loads(p.stdout.strip().splitlines()[-1])
+    assert res == {"logical_devices": ndev, "gzip_equal": True, "raw_equal": True, "oracle_ok": True,
+                   "crc_ok": True}, res

@@ -125,3 +125,33 @@ def test_resume_at_bit_offset_with_window(oracle):
     out2, end2, fin2 = ztamd.inflate_raw_resume(s, end1, out1)
     assert fin2 and out1 + out2 == data
     assert (end2 + 7) // 8 == len(s)
+
+
+def test_finish_reports_corrupt_tail(oracle):
+    """A stream that has fully arrived but is corrupt in its last 8 bytes:
+    decompress() keeps waiting for more input (the error is within the last
+    64 bits), finish() -- the caller has no more input -- raises the
+    stream's own error, as a one-shot decode does.  A truncated stream
+    (no final block) raises on finish() too; a valid one finishes."""
+    import ztamd
+
+    data = oracle.gen("wordsalad", 21, 200_000)
+    good = raw(data)
+    st = ztamd.RawInflateStream()
+    assert st.finish(good) == data and st.bfinal
+    # the whole text, a sync flush, then a final stored block whose NLEN is
+    # not ~LEN: the error lies in the last 10 bytes
+    c = zlib.compressobj(6, zlib.DEFLATED, -15)
+    bad = c.compress(data) + c.flush(zlib.Z_SYNC_FLUSH) + b"\x01\x05\x00\x00\x00hello"
+    with pytest.raises(ztamd.ZtError):
+        ztamd.inflate_raw(bad)  # the one-shot decode rejects it
+    st = ztamd.RawInflateStream()
+    st.decompress(bad)
+    assert not st.bfinal  # still waiting for input
+    with pytest.raises(ztamd.ZtError):
+        st.finish()
+    st = ztamd.RawInflateStream()
+    part = st.decompress(good[: len(good) // 2])
+    with pytest.raises(ztamd.ZtError):
+        st.finish()
+    assert data.startswith(part)

@@ -112,3 +112,40 @@ def test_zip_many_files_roundtrip(zt, oracle):
     with zipfile.ZipFile(io.BytesIO(arch)) as zf:
         assert zf.testzip() is None
         assert [zf.read(f"f{i:03d}") for i in range(300)] == [f["data"] for f in files]
+
+
+def test_unzip_data_descriptor(zt, oracle):
+    """Archives with data descriptors (general-purpose flag bit 3, local CRC and
+    sizes 0 -- what a writer on a non-seekable stream emits): every DEFLATE
+    member, including ones far larger than 64 KiB compressed, decodes from
+    its offset as the reference's RawInflate would (src/Unzip.ts:284-288).
+    The reference itself never returns on such archives (its RawInflate gets
+    bufferSize 0, tools/gen_golden_zip.mjs), so this is pinned by Python's
+    zipfile, which wrote them."""
+    import io
+    import zipfile
+
+    class Sink(io.RawIOBase):
+        def __init__(self):
+            self.buf = bytearray()
+
+        def writable(self):
+            return True
+
+        def write(self, b):
+            self.buf += b
+            return len(b)
+
+    data = [oracle.gen("xorshift32", 31, 300000), oracle.gen("wordsalad", 32, 200000),
+            oracle.gen("structured", 33, 150000), b"", b"tail"]
+    sink = Sink()
+    with zipfile.ZipFile(sink, "w", zipfile.ZIP_DEFLATED) as zf:
+        for i, d in enumerate(data):
+            zf.writestr(f"m{i}", d)
+    arch = bytes(sink.buf)
+    entries = parse_zip(arch)["entries"]
+    assert all(e["flags"] & 8 for e in entries)
+    assert max(e["compressed_size"] for e in entries) > 65536 + 1024
+    err, ents = zt.unzip(arch, verify=False)
+    assert err is None
+    assert [e["data"] for e in ents] == data

@@ -5,9 +5,9 @@
   C3  RawDeflate level 6 of one 8 GiB device-resident buffer (deflate only), ratio
   C4  GZip of 10,000 mixed text/binary files (1-64 KiB) through the host API
       zt_gzip_compress (PCIe included), members checked by GUnzip
-Streams for C2 are single-block raw DEFLATE of 64 KiB pieces produced by the
-oracle's restatement of the reference RawDeflate (src/RawDeflate.ts: one
-dynamic block per input), 64 distinct pieces replicated to 4096."""
+Streams for C2 are SURVEY 8(d)'s 4096 distinct blocks (tests/c2_corpus.py:
+even i xorshift32(100 + i), odd i wordsalad(100 + i), each deflated by the
+oracle's byte-exact restatement of the reference RawDeflate)."""
 import os, sys, time, json
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, '..', 'zlib.ts_amd', 'py')); sys.path.insert(0, os.path.join(HERE, '..', 'tests'))
@@ -29,18 +29,14 @@ dt = (time.perf_counter() - t0) / 10
 res["C1_checksums_GiBps"] = round(n / dt / 2**30, 2)
 res["C1_checksums_frac_hbm"] = round(n / dt / 8e12, 3)
 del d
-# C2
+# C2: SURVEY 8(d)'s workload -- 4096 distinct reference-deflated 64 KiB blocks
+# (tests/c2_corpus.py; the device-side kernel times: tools/c2_bench.py under rocprofv3)
 o = zt_oracle.Oracle()
-pieces = []
-for i in range(64):
-    kind = ["wordsalad", "structured", "xorshift32"][i % 3]
-    raw = o.gen(kind, 500 + i, 65536)
-    s, _ = o.raw_deflate(raw)
-    pieces.append((raw, s))
-items = [pieces[i % 64] for i in range(4096)]
-streams = [s for _, s in items]
+import c2_corpus
+corpus = c2_corpus.build(o)
+streams = [s for _, s, _ in corpus]
 out = zt.inflate_raw_batch(streams)
-assert all(st == 0 and ob == raw for (raw, _), (st, ob, ip) in zip(items, out))
+assert all(st == 0 and ob == raw for (raw, _, _), (st, ob, ip) in zip(corpus, out))
 t0 = time.perf_counter()
 for _ in range(3):
     zt.inflate_raw_batch(streams)

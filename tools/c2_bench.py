@@ -1,0 +1,47 @@
+"""Config C2 measured at its own workload: zt_inflate_raw_batch
+of the 4096 distinct reference-deflated 64 KiB blocks of tests/c2_corpus.py.
+
+Prints one JSON line: the host-API rate (C call: pinned packing, H2D, the
+batch kernels, D2H and the output slab included) and, with ZT_BATCH_TIMING=1,
+the stage split on stderr.  Run under `rocprofv3 --kernel-trace --stats` for
+the device-side kernel times (sum of the batch kernels / CALLS = the device
+time of one call; profiles/r03*_c2_*).
+   usage: python tools/c2_bench.py [calls]
+"""
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "zlib.ts_amd", "py"))
+sys.path.insert(0, os.path.join(HERE, "..", "tests"))
+import c2_corpus  # noqa: E402
+import ztamd as zt  # noqa: E402
+import zt_oracle  # noqa: E402
+
+calls = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+t0 = time.perf_counter()
+corpus = c2_corpus.build(zt_oracle.Oracle())
+t_build = time.perf_counter() - t0
+streams = [s for _, s, _ in corpus]
+out = zt.inflate_raw_batch(streams)  # warm + check
+ok = all(st == 0 and ob == raw and ip == len(s) for (raw, s, _), (st, ob, ip) in zip(corpus, out))
+if not ok:
+    raise SystemExit("c2_bench: mismatch")
+ts = []
+for _ in range(calls):
+    t0 = time.perf_counter()
+    zt.inflate_raw_batch(streams)
+    ts.append(time.perf_counter() - t0)
+nbytes = c2_corpus.COUNT * c2_corpus.BLOCK
+print(json.dumps({
+    "config": "C2: zt_inflate_raw_batch of 4096 distinct reference-deflated 64 KiB blocks "
+              "(even i xorshift32(100+i), odd i wordsalad(100+i))",
+    "calls": calls,
+    "input_MiB": round(sum(len(s) for s in streams) / 2**20, 2),
+    "output_MiB": nbytes / 2**20,
+    "host_api_ms_median": round(sorted(ts)[len(ts) // 2] * 1e3, 2),
+    "host_api_GiBps": round(nbytes / sorted(ts)[len(ts) // 2] / 2**30, 3),
+    "corpus_build_s": round(t_build, 1),
+}), flush=True)

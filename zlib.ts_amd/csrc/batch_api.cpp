@@ -154,7 +154,7 @@ int batch_grouped(DeviceCtx *c, const uint8_t *const *in, const std::vector<size
     cv.wait(lk, [&] { return counter > g || err; });
     return err == 0;
   };
-  const int dev = c->device;
+  const int dev = c->phys;
   auto up_stage = [&]() -> int {
     ZT_HIP(hipSetDevice(dev));
     for (size_t g = 0; g < ng; ++g) {

@@ -212,7 +212,7 @@ int zt_inflate_dev(zt_inflate_plan *plan, const void *d_in, size_t n, void *d_ou
   uint8_t *o = (uint8_t *)d_out;
   size_t ol = 0, eip = 0;
   int seg = inflate_segments_dev(c, (const uint8_t *)d_in, n, 0, &o, out_cap, &ol, &eip, s);
-  if (seg == 1) seg = inflate_general_dev(c, (const uint8_t *)d_in, n, 0, &o, out_cap, &ol, &eip, s);
+  if (seg >= 1) seg = inflate_general_dev(c, (const uint8_t *)d_in, n, 0, &o, out_cap, &ol, &eip, s);
   if (seg < 0) return seg;
   if (seg == 0) {
     *out_len = ol;

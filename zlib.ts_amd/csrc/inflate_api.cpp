@@ -207,8 +207,9 @@ static int inflate_dev_batch(DeviceCtx *c, const void *d_in, const std::vector<s
                              size_t *end_ip, int *status) {
   std::vector<size_t> cap(count);
   for (size_t i = 0; i < count; ++i) {
-    // first guess; exact sizes are known after one pass
-    size_t g = n[i] * 4;
+    // first guess (4x the stream's bytes from its start); exact sizes are
+    // known after one pass
+    size_t g = 4 * (n[i] - std::min(n[i], index ? index[i] : (size_t)0));
     cap[i] = g < 65536 ? 65536 : g;
   }
   void *d_jobs, *d_res;
@@ -345,7 +346,10 @@ int inflate_dev_member(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t index
       uint8_t *d_out = nullptr;
       size_t ol = 0, eip = 0;
       int seg = inflate_segments_dev(c, d_in, ne, index, &d_out, 0, &ol, &eip, s);
-      if (seg == 1) seg = inflate_general_dev(c, d_in, ne, index, &d_out, 0, &ol, &eip, s);
+      // the window cut a stream with sync points short (2): grow it, no
+      // general-path attempt (it cannot finish inside the window either)
+      if (seg == 2 && ne < n) continue;
+      if (seg >= 1) seg = inflate_general_dev(c, d_in, ne, index, &d_out, 0, &ol, &eip, s);
       if (seg < 0) return seg;
       if (seg == 0) {
         uint8_t *h = host_out(ol);
@@ -389,7 +393,7 @@ int zt_inflate_raw(const uint8_t *in, size_t n, size_t index, const zt_inflate_o
     size_t ol = 0, eip = 0;
     int seg = inflate_segments_dev(c, (const uint8_t *)d_in, n, index, &d_out, 0, &ol, &eip, c->stream);
     // no sync points: speculative parallel decode at arbitrary bit offsets
-    if (seg == 1) seg = inflate_general_dev(c, (const uint8_t *)d_in, n, index, &d_out, 0, &ol, &eip, c->stream);
+    if (seg >= 1) seg = inflate_general_dev(c, (const uint8_t *)d_in, n, index, &d_out, 0, &ol, &eip, c->stream);
     if (seg < 0) return seg;
     if (seg == 0) {
       uint8_t *h = host_out(ol);
@@ -413,8 +417,12 @@ int zt_inflate_raw(const uint8_t *in, size_t n, size_t index, const zt_inflate_o
   return rc;
 }
 
-int zt_inflate_raw_resume(const uint8_t *in, size_t n, uint64_t bit_pos, const uint8_t *window, size_t wlen,
-                          uint8_t **out, size_t *out_len, uint64_t *end_bits, int *finished) {
+}  // extern "C"
+
+// zt_inflate_raw_resume / _final: `final_input` = the caller has no more
+// input, so every kernel status is the stream's own (running out is an error)
+static int resume_impl(const uint8_t *in, size_t n, uint64_t bit_pos, const uint8_t *window, size_t wlen,
+                       uint8_t **out, size_t *out_len, uint64_t *end_bits, int *finished, int final_input) {
   if (!out || !out_len || !end_bits || !finished) return set_error(ZT_E_ARG, "null output");
   if ((n && !in) || (wlen && !window)) return set_error(ZT_E_ARG, "null input");
   if (bit_pos > (uint64_t)n * 8) return set_error(ZT_E_ARG, "bit position past the end of the input");
@@ -465,9 +473,9 @@ int zt_inflate_raw_resume(const uint8_t *in, size_t n, uint64_t bit_pos, const u
     // running out of input (the reader's end-of-input statuses, or any error
     // within the last 64 bits, where a peek may have seen the zeros past the
     // end) means "more input needed"; an error before that is the stream's own
-    const bool truncated = r.status == ZT_E_INPUT_BROKEN || r.status == ZT_E_STORED_LEN ||
-                           r.status == ZT_E_STORED_NLEN || r.status == ZT_E_INVALID_CODE_LENGTH ||
-                           r.stop_bits + 64 > (uint64_t)m * 8;
+    const bool truncated = !final_input && (r.status == ZT_E_INPUT_BROKEN || r.status == ZT_E_STORED_LEN ||
+                                            r.status == ZT_E_STORED_NLEN || r.status == ZT_E_INVALID_CODE_LENGTH ||
+                                            r.stop_bits + 64 > (uint64_t)m * 8);
     if (r.status != ZT_OK && !truncated) return inflate_error(r.status, r.detail);
     const uint64_t done = (r.status == ZT_OK ? r.out_len : r.blk_op) - wlen;  // new bytes
     if (done > cap) {  // decoded past the output guess: again with the exact size
@@ -488,6 +496,18 @@ int zt_inflate_raw_resume(const uint8_t *in, size_t n, uint64_t bit_pos, const u
     return ZT_OK;
   }
   return set_error(ZT_E_INTERNAL, "resume: output size did not settle");
+}
+
+extern "C" {
+
+int zt_inflate_raw_resume(const uint8_t *in, size_t n, uint64_t bit_pos, const uint8_t *window, size_t wlen,
+                          uint8_t **out, size_t *out_len, uint64_t *end_bits, int *finished) {
+  return resume_impl(in, n, bit_pos, window, wlen, out, out_len, end_bits, finished, 0);
+}
+
+int zt_inflate_raw_resume_final(const uint8_t *in, size_t n, uint64_t bit_pos, const uint8_t *window, size_t wlen,
+                                uint8_t **out, size_t *out_len, uint64_t *end_bits, int *finished) {
+  return resume_impl(in, n, bit_pos, window, wlen, out, out_len, end_bits, finished, 1);
 }
 
 int zt_inflate_raw_batch(const uint8_t *const *in, const size_t *n, size_t count, const zt_inflate_opts *opts,

@@ -306,6 +306,13 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   size_t u = 0;
   for (;;) {
     const TokResult &r = res[u];
+    // the chain reached the last unit (which runs to the end of the input)
+    // and that one ran out of input: a window that cuts a longer stream
+    // (inflate_dev_member grows it) -- or a truncated stream
+    if (u + 1 == units && u > 0 && (r.status == ZT_E_INPUT_BROKEN || r.status == ZT_E_STORED_LEN)) {
+      if (inf_debug()) fprintf(stderr, "[zt inflate] chain ran out of input in its last unit %zu\n", u);
+      return 2;
+    }
     if (r.status != ZT_OK || r.out_len > 0xFFFFFFFFull)
       FALLBACK("unit %zu (chain %zu): status %d detail %d ntok %u out %llu\n", u, chain.size(), r.status,
                r.detail, r.ntok, (unsigned long long)r.out_len);

@@ -76,7 +76,8 @@ int zt_zip_compress(const uint8_t *const *in, const size_t *n, const zt_zip_file
   } freer{body};
   std::vector<size_t> defl, stored;
   for (size_t i = 0; i < count; ++i) {
-    if (files[i].method != 0 && files[i].method != 8) return set_error(ZT_E_ARG, "unsupported compression method");
+    // only DEFLATE (8) is compressed; any other method number is stored
+    // as-is and written unchanged into both headers (src/Zip.ts:92,146,255)
     (files[i].method == 8 ? defl : stored).push_back(i);
   }
   while (!defl.empty()) {
@@ -235,6 +236,7 @@ int zt_unzip(const uint8_t *in, size_t n, int verify, uint8_t **out, size_t *out
   if ((uint64_t)cd_size < c.p - (uint64_t)cd_off) return set_error(ZT_E_ZIP_FORMAT, "invalid file header size");
   // local headers: src/Unzip.ts:28-62, 248-291
   std::vector<size_t> doff(total, 0), dlen(total, 0);
+  std::vector<char> open_end(total, 0);
   std::vector<size_t> defl;
   for (uint32_t i = 0; i < total; ++i) {
     zt_unzip_entry &e = ent[i];
@@ -263,6 +265,10 @@ int zt_unzip(const uint8_t *in, size_t n, int verify, uint8_t **out, size_t *out
     }
     doff[i] = l.p;
     dlen[i] = csize;
+    // a data descriptor (flag bit 3) leaves the local size 0: such a member's
+    // stream is bounded by nothing before the input's end, as in the
+    // reference's RawInflate from the member's offset (src/Unzip.ts:284-288)
+    open_end[i] = (flags & 8) != 0 || csize == 0;
     if (method == 8) defl.push_back(i);
   }
   // every DEFLATE member inflated in one batch (RawInflate from the member's
@@ -283,15 +289,16 @@ int zt_unzip(const uint8_t *in, size_t n, int verify, uint8_t **out, size_t *out
     ZT_TRY(scratch(dc, 19, n + 64, &d_in));
     ZT_TRY(upload(dc, d_in, in, n, dc->stream));
     const size_t m = defl.size();
-    // (each member's input ends 64 KiB past its compressed size: a valid
-    // member's stream ends inside it; the reference reads on into the next
-    // bytes only for a corrupt member)
+    // (a member with a known compressed size reads at most 64 KiB past it:
+    // a valid stream ends inside, and only a corrupt one would read on into
+    // the next bytes; a member without one -- data descriptor -- reads to
+    // the input's end)
     std::vector<size_t> in_off(m, 0), nn(m, n), idx(m), bl(m), eip(m);
     std::vector<uint8_t *> bp(m, nullptr);
     std::vector<int> st(m, 0);
     for (size_t k = 0; k < m; ++k) {
       idx[k] = std::min(doff[defl[k]], n);
-      nn[k] = std::min<size_t>(n, idx[k] + dlen[defl[k]] + (64u << 10));
+      nn[k] = open_end[defl[k]] ? n : std::min<size_t>(n, idx[k] + dlen[defl[k]] + (64u << 10));
     }
     (void)inflate_batch_dev_streams(dc, d_in, in_off, nn.data(), idx.data(), m, bp.data(), bl.data(), eip.data(),
                                     st.data());

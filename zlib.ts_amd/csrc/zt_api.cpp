@@ -59,22 +59,43 @@ int timing_collect(DeviceCtx *c, double *acc_ms, uint64_t *count, int k) {
 static std::mutex g_mu;
 static std::vector<DeviceCtx *> g_ctx;
 
-int get_ctx(DeviceCtx **out) {
+// Test-only rehearsal of a multi-GPU node on fewer GPUs: ZT_ALIAS_DEVICES=k
+// (read once) makes the library present k logical devices, logical d running
+// on HIP device d % (HIP device count) with its own context (streams,
+// scratch, pinned staging, host threads) -- what zt_set_devices(mask) spreads
+// a batch over.  Unset: logical = HIP devices.
+static int hip_count() {
   int count = 0;
-  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
-    return set_error(ZT_E_NO_DEVICE, "no HIP device visible (libzt computes on the GPU only)");
+  if (hipGetDeviceCount(&count) != hipSuccess) return 0;
+  return count;
+}
+static int alias_count() {
+  static const int k = [] {
+    const char *e = getenv("ZT_ALIAS_DEVICES");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 && v <= 64 ? v : 0;
+  }();
+  return k;
+}
+
+int get_ctx(DeviceCtx **out) {
+  const int hc = hip_count();
+  if (hc <= 0) return set_error(ZT_E_NO_DEVICE, "no HIP device visible (libzt computes on the GPU only)");
+  const int count = alias_count() ? alias_count() : hc;
   if (g_dev < 0 || g_dev >= count) return set_error(ZT_E_NO_DEVICE, "invalid device index");
+  const int phys = g_dev % hc;
   std::lock_guard<std::mutex> lk(g_mu);
   if (g_ctx.size() < (size_t)count) g_ctx.resize(count, nullptr);
-  ZT_HIP(hipSetDevice(g_dev));
+  ZT_HIP(hipSetDevice(phys));
   if (!g_ctx[g_dev]) {
     DeviceCtx *c = new DeviceCtx();
     c->device = g_dev;
+    c->phys = phys;
     ZT_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     ZT_HIP(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
     ZT_HIP(hipEventCreateWithFlags(&c->aux_ev, hipEventDisableTiming));
     hipDeviceProp_t prop;
-    ZT_HIP(hipGetDeviceProperties(&prop, g_dev));
+    ZT_HIP(hipGetDeviceProperties(&prop, phys));
     c->num_cu = prop.multiProcessorCount;
     uint32_t bt[256], nib[ZT_CRC_NIB_N], x2n[32];
     crc_host_tables(bt, nib, x2n);
@@ -295,7 +316,7 @@ int pipeline_h2d_d2h(DeviceCtx *c, size_t np, const std::function<PipePiece(size
     std::lock_guard<std::mutex> lk(mu);
     return err != 0;
   };
-  const int dev = c->device;
+  const int dev = c->phys;
   // stage 1: host -> pinned chunk (host threads) -> device (DMA on c->up)
   auto up_stage = [&]() -> int {
     ZT_HIP(hipSetDevice(dev));
@@ -434,9 +455,8 @@ int zt_set_devices(uint64_t mask) {
 }
 
 int zt_device_count(void) {
-  int count = 0;
-  if (hipGetDeviceCount(&count) != hipSuccess) return 0;
-  return count;
+  const int hc = hip_count();
+  return hc > 0 && alias_count() ? alias_count() : hc;
 }
 
 int zt_set_device(int device) {

@@ -36,7 +36,8 @@ struct DeviceCtx {
   // host entry points hold it for their whole call: scratch, pinned staging
   // and the streams are shared by every thread that uses this device
   std::recursive_mutex mu;
-  int device = -1;
+  int device = -1;  // logical device (zt_set_device index)
+  int phys = -1;    // HIP device it runs on (differs only under ZT_ALIAS_DEVICES)
   hipStream_t stream = nullptr;
   int num_cu = 0;
   // checksum constants (uploaded once)

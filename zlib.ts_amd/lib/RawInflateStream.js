@@ -25,12 +25,26 @@ export class RawInflateStream {
     }
 
     decompress(newInput, ip) {
+        return this._run(newInput, ip, 0);
+    }
+
+    // The input is complete (no more will come): decodes what is left and
+    // throws the reference's message when the stream is corrupt near its end
+    // or ends before its final block (decompress() would wait for more input).
+    finish(newInput, ip) {
+        const out = this._run(newInput, ip, 1);
+        if (!this.bfinal) throw new Error('input buffer is broken');
+        return out;
+    }
+
+    _run(newInput, ip, finalInput) {
         if (newInput) this.input = newInput instanceof Uint8Array ? newInput : new Uint8Array(newInput);
         this.ip = dflt(ip, this.ip);
-        if (this.bfinal || this.ip >= this.input.length) return new Uint8Array(0);
+        if (this.bfinal) return new Uint8Array(0);
+        if (this.ip >= this.input.length && !finalInput) return new Uint8Array(0);
         let r;
         try {
-            r = native.inflateResume(this.input, this.ip * 8 + this.bitpos, this.window);
+            r = native.inflateResume(this.input, this.ip * 8 + this.bitpos, this.window, finalInput);
         } catch (e) {
             throw refError(e);
         }

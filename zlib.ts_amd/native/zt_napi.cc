@@ -170,10 +170,11 @@ void set_num(napi_env env, napi_value obj, const char *k, double v) {
   napi_set_named_property(env, obj, k, x);
 }
 
-// inflateResume(input: Uint8Array, bitPos, window: Uint8Array) -> {output, endBits, finished}
+// inflateResume(input: Uint8Array, bitPos, window: Uint8Array[, final]) -> {output, endBits, finished}
+// (final: no more input will come -- zt_inflate_raw_resume_final)
 napi_value inflate_resume(napi_env env, napi_callback_info info) {
-  napi_value a[3];
-  args(env, info, a, 3);
+  napi_value a[4];
+  args(env, info, a, 4);
   const uint8_t *p, *w;
   size_t n, wn;
   if (!get_u8(env, a[0], &p, &n) || !get_u8(env, a[2], &w, &wn)) return nullptr;
@@ -182,7 +183,9 @@ napi_value inflate_resume(napi_env env, napi_callback_info info) {
   size_t olen = 0;
   uint64_t end = 0;
   int fin = 0;
-  int rc = zt_inflate_raw_resume(p, n, bit < 0 ? 0 : (uint64_t)bit, w, wn, &out, &olen, &end, &fin);
+  const bool final_input = get_i64(env, a[3], 0) != 0;
+  int rc = (final_input ? zt_inflate_raw_resume_final : zt_inflate_raw_resume)(p, n, bit < 0 ? 0 : (uint64_t)bit, w,
+                                                                               wn, &out, &olen, &end, &fin);
   if (rc) return throw_zt(env, rc);
   napi_value obj, f;
   napi_create_object(env, &obj);

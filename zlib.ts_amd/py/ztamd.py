@@ -103,6 +103,8 @@ def _load():
         "zt_inflate_raw": ([vp, sz, sz, P(InflateOpts), u8pp, P(sz), P(sz)], ctypes.c_int),
         "zt_inflate_raw_resume": ([vp, sz, ctypes.c_uint64, vp, sz, u8pp, P(sz), P(ctypes.c_uint64),
                                    P(ctypes.c_int)], ctypes.c_int),
+        "zt_inflate_raw_resume_final": ([vp, sz, ctypes.c_uint64, vp, sz, u8pp, P(sz), P(ctypes.c_uint64),
+                                         P(ctypes.c_int)], ctypes.c_int),
         "zt_inflate_raw_batch": ([P(vp), P(sz), sz, P(InflateOpts), u8pp, P(sz), P(sz), P(ctypes.c_int)],
                                  ctypes.c_int),
         "zt_deflate_raw_batch": ([P(vp), P(sz), sz, P(DeflateOpts), u8pp, P(sz), P(ctypes.c_int)], ctypes.c_int),
@@ -142,7 +144,8 @@ lib = _load()
 # every symbol include/zt.h declares (checked by tests/test_abi.py)
 SYMBOLS = [
     "zt_device_count", "zt_set_device", "zt_set_devices", "zt_last_error_message", "zt_version", "zt_free", "zt_crc32_update",
-    "zt_adler32_update", "zt_checksums", "zt_deflate_raw", "zt_inflate_raw", "zt_inflate_raw_resume", "zt_inflate_raw_batch",
+    "zt_adler32_update", "zt_checksums", "zt_deflate_raw", "zt_inflate_raw", "zt_inflate_raw_resume", "zt_inflate_raw_resume_final",
+    "zt_inflate_raw_batch",
     "zt_deflate_raw_batch", "zt_gzip_compress", "zt_gzip_compress_batch", "zt_zlib_compress_batch", "zt_gunzip",
     "zt_crc32_batch", "zt_zip_compress", "zt_unzip", "zt_zlib_compress", "zt_zlib_decompress",
     "zt_dev_checksums", "zt_deflate_plan_create", "zt_deflate_plan_destroy",
@@ -220,16 +223,18 @@ def inflate_raw(data, index=0, ref_strict=False, buffer_type=1, buffer_size=0x80
     return res, ip.value
 
 
-def inflate_raw_resume(data, bit_pos=0, window=b""):
-    """zt_inflate_raw_resume: (output of the complete blocks, end bit, finished)."""
+def inflate_raw_resume(data, bit_pos=0, window=b"", final=False):
+    """zt_inflate_raw_resume (final: zt_inflate_raw_resume_final -- no more
+    input will come, errors are the stream's own): (output of the complete
+    blocks, end bit, finished)."""
     b, n = _cbuf(data)
     w, wn = _cbuf(window)
     out = ctypes.POINTER(ctypes.c_uint8)()
     olen = ctypes.c_size_t()
     end = ctypes.c_uint64()
     fin = ctypes.c_int()
-    _check(lib.zt_inflate_raw_resume(b, n, bit_pos, w, wn, ctypes.byref(out), ctypes.byref(olen), ctypes.byref(end),
-                                     ctypes.byref(fin)))
+    fn = lib.zt_inflate_raw_resume_final if final else lib.zt_inflate_raw_resume
+    _check(fn(b, n, bit_pos, w, wn, ctypes.byref(out), ctypes.byref(olen), ctypes.byref(end), ctypes.byref(fin)))
     res = ctypes.string_at(out, olen.value) if out else b""
     if out:
         lib.zt_free(out)
@@ -252,13 +257,24 @@ class RawInflateStream:
         self.total = 0
 
     def decompress(self, new_input=None, ip=None):
+        return self._run(new_input, ip, False)
+
+    def finish(self, new_input=None, ip=None):
+        """The input is complete: decode what is left; a stream corrupt near
+        its end, or one that ends before its final block, raises ZtError."""
+        out = self._run(new_input, ip, True)
+        if not self.bfinal:
+            raise ZtError(-10, "input buffer is broken")
+        return out
+
+    def _run(self, new_input, ip, final):
         if new_input is not None:
             self.input = bytes(new_input)
         if ip is not None:  # (a re-based buffer: the bits of its byte `ip` already used stay used)
             self.ip = ip
-        if self.bfinal or self.ip >= len(self.input):
+        if self.bfinal or (self.ip >= len(self.input) and not final):
             return b""
-        out, end, fin = inflate_raw_resume(self.input, self.ip * 8 + self.bit, self.window)
+        out, end, fin = inflate_raw_resume(self.input, self.ip * 8 + self.bit, self.window, final)
         self.ip, self.bit = end >> 3, end & 7
         self.bfinal = fin
         self.total += len(out)
