@@ -139,17 +139,18 @@ def test_finish_reports_corrupt_tail(oracle):
     good = raw(data)
     st = ztamd.RawInflateStream()
     assert st.finish(good) == data and st.bfinal
-    # the whole text, a sync flush, then a final stored block whose NLEN is
-    # not ~LEN: the error lies in the last 10 bytes
+    # the whole text, a sync flush, then a final block of BTYPE 3 ("unknown
+    # BTYPE: 3", src/RawInflate.ts:168): the error lies in the last 2 bytes
     c = zlib.compressobj(6, zlib.DEFLATED, -15)
-    bad = c.compress(data) + c.flush(zlib.Z_SYNC_FLUSH) + b"\x01\x05\x00\x00\x00hello"
+    bad = c.compress(data) + c.flush(zlib.Z_SYNC_FLUSH) + b"\x07\x00"
     with pytest.raises(ztamd.ZtError):
         ztamd.inflate_raw(bad)  # the one-shot decode rejects it
     st = ztamd.RawInflateStream()
     st.decompress(bad)
     assert not st.bfinal  # still waiting for input
-    with pytest.raises(ztamd.ZtError):
+    with pytest.raises(ztamd.ZtError) as e:
         st.finish()
+    assert e.value.msg == "unknown BTYPE: 3"
     st = ztamd.RawInflateStream()
     part = st.decompress(good[: len(good) // 2])
     with pytest.raises(ztamd.ZtError):

@@ -2,27 +2,27 @@
 // one HBM pass (replaces src/CRC32.ts:25-47 and src/Adler32.ts:28-48).
 //
 // Decomposition (HBM-bound byte work; no MFMA):
-//   * the input is cut into 256 KiB segments, one 256-thread workgroup each
-//     (grid-stride), 64 KiB per wave (ZT_CK_THREADS / ZT_CK_B: 512 threads
-//     0.63 ms, 256 threads with 4 / 8 / 16 rows per batch 0.44 / 0.41-0.43
-//     / 0.49 ms per GiB);
-//   * loads are coalesced: each wave instruction reads 1 KiB contiguous, lane l
-//     the 16 bytes at 16 l; a row is CK_Q such loads, so lane l's bytes are
-//     CK_P = 16 CK_Q-byte pieces CK_RB = 64 CK_P bytes apart.
-//     Its CRC is kept as a lane stream: L <- L * x^(8 * CK_RB) + raw(piece)
-//     (raw: the piece's CRC from state 0, slice-by-8 steps; the multiplication
-//     by the constant: 8 lookups in nibble tables of x^(8 * CK_RB) * v), and
-//     each lane stream is moved to the segment end once, by one
-//     multiplication (earlier design: one contiguous 1 KiB slice per lane,
-//     64 cache lines per load instruction and no L1 reuse, 23 % of HBM);
-//   * CRC lookups: nibble tables, each replicated 32x in LDS so that lane l
-//     always reads bank l -- every ds_read_b32 is conflict-free (2.25
-//     lookups/byte); one v_perm_b32 per lookup address, 3-input XORs
-//     (v_bitop3_b32);  Adler: v_dot4_u32_u8 sums per piece, positions weighted
-//     from the piece's place in the segment;
+//   * the input is cut into CK_SEG-byte segments (512 KiB), one 256-thread
+//     workgroup each (grid-stride), CK_SEG / 4 contiguous bytes per wave;
+//   * loads are coalesced: each wave instruction reads 1 KiB contiguous, lane
+//     l the 16 bytes at 16 l; a row is 8 such loads (8 KiB per wave), so a
+//     lane holds 32 words per row, word j = 4 q + w at 1024 q + 16 l + 4 w;
+//   * CRC-32, table-free and bit-sliced: the lane runs 32 streams (stream j =
+//     word j of every row) in 32 registers P[0..31], P[b] holding state bit
+//     b of all 32 streams.  Per row the 32 data words are transposed into the
+//     same form (16 v_perm_b32 + 96 v_bfi_b32 pairs' worth of selects) and
+//     the streams advance by one row: P <- A P ^ D, A = multiplication by
+//     x^(8 * 8192) mod P, a constant 32 x 32 GF(2) matrix unrolled at compile
+//     time into 3-input XORs (v_bitop3_b32) -- about 4 VALU per byte, no
+//     LDS; the 32 streams then fold pairwise into one (streams 16 apart are
+//     4 KiB apart: P <- M P ^ (P >> 16), then 8, 4, 2, 1) and the lane's CRC
+//     moves to the segment end by one multiplication;
+//   * Adler: v_dot4_u32_u8 sums per 16-byte piece, positions weighted from
+//     the piece's place in the segment;
 //   * per-lane results are merged with polynomial shifts (CRC) and weighted
 //     sums (Adler) inside the workgroup, then one tiny kernel merges segments.
-//     Ragged first / last segments take a byte-wise per-thread-slice path.
+//     Ragged first / last segments take a byte-wise per-thread-slice path
+//     (slice-by-8 through nibble tables in LDS).
 // Algorithmic bytes per unit: N input bytes read.
 #include <vector>
 
@@ -35,23 +35,19 @@ namespace {
 #ifndef ZT_CK_THREADS
 #define ZT_CK_THREADS 256
 #endif
-#ifndef ZT_CK_Q
-#define ZT_CK_Q 2  // 16-byte loads per lane per row: a lane's piece of a row is 16 Q contiguous bytes
+#ifndef ZT_CK_ROWS
+#define ZT_CK_ROWS 16  // 8 KiB rows per wave: a segment is 4 waves x ZT_CK_ROWS x 8 KiB
 #endif
-#ifndef ZT_CK_B
-#define ZT_CK_B (8 / ZT_CK_Q)  // rows per batch (8 loads per lane in flight)
+#ifndef ZT_CK_MINW
+#define ZT_CK_MINW 2  // waves per SIMD the register allocation must allow (4: 128 VGPRs, spills)
 #endif
-constexpr int CK_THREADS = ZT_CK_THREADS;            // 4 waves per workgroup, 3 workgroups per CU (LDS)
-constexpr int CK_SLICE = 262144 / CK_THREADS;        // bytes per thread (ragged segments)
-constexpr size_t CK_SEG = (size_t)CK_THREADS * CK_SLICE;  // 256 KiB per segment
-constexpr int NIB_ENTRIES = ZT_CRC_NIB_N;            // (16 + 8) nibble positions x 16 values
-constexpr int ADV = 16;                              // first nibble table of x^(8*1024) * v
-constexpr int CK_WAVE_BYTES = 262144 / (CK_THREADS / 64);  // contiguous bytes per wave in a whole segment
-constexpr int CK_Q = ZT_CK_Q;
-constexpr int CK_P = 16 * CK_Q;   // a lane's contiguous bytes per row
-constexpr int CK_RB = 64 * CK_P;  // bytes per row (one wave: 64 lanes x CK_P)
-static_assert(CK_WAVE_BYTES % (CK_RB * ZT_CK_B) == 0, "rows tile the wave's bytes");
-static_assert(CK_WAVE_BYTES * (CK_THREADS / 64) == (int)CK_SEG, "waves tile the segment");
+constexpr int CK_THREADS = ZT_CK_THREADS;
+constexpr int CK_ROWS = ZT_CK_ROWS;
+constexpr int CK_ROW = 8192;                                   // bytes per row (one wave: 8 x 1 KiB loads)
+constexpr int CK_WAVE_BYTES = CK_ROWS * CK_ROW;                // contiguous bytes per wave in a whole segment
+constexpr size_t CK_SEG = (size_t)CK_WAVE_BYTES * (CK_THREADS / 64);
+constexpr int CK_SLICE = (int)(CK_SEG / CK_THREADS);          // bytes per thread (ragged segments)
+static_assert(CK_THREADS % 64 == 0 && CK_SLICE % 128 == 0, "geometry");
 
 // batch checksums: segment k of the buffer at frame + off (off 16-byte aligned)
 struct CkJob {
@@ -116,11 +112,115 @@ __device__ __forceinline__ uint32_t crc_step8(uint32_t c, uint32_t w0, uint32_t 
   return xor3(x0, x1, x2) ^ xor3(x3, x4, t[7]);
 }
 
-// c * x^(8 * CK_RB) mod P (the lane stream's advance by one row), xor x
-__device__ __forceinline__ uint32_t crc_adv1k(uint32_t c, uint32_t x, const uint32_t *T, uint32_t lb) {
-  uint32_t t[8];
-  lut8<ADV>(c, T, lb, t);
-  return xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), xor3(t[6], t[7], x));
+// ---- bit-sliced CRC-32 ----------------------------------------------------
+// GF(2) arithmetic of zlib's multmodp convention (x^0 = bit 31), at compile
+// time: the matrices below are folded into the instruction stream.
+constexpr uint32_t cx_mult(uint32_t a, uint32_t b) {
+  uint32_t p = 0;
+  for (int i = 31; i >= 0; --i) {
+    if ((a >> i) & 1u) p ^= b;
+    b = (b & 1u) ? (b >> 1) ^ ZT_CRC_POLY : b >> 1;
+  }
+  return p;
+}
+constexpr uint32_t cx_x8n(uint64_t n) {  // x^(8 n) mod P
+  uint32_t p = 1u << 31, base = 1u << 23;
+  while (n) {
+    if (n & 1u) p = cx_mult(base, p);
+    base = cx_mult(base, base);
+    n >>= 1;
+  }
+  return p;
+}
+struct GfMat {
+  uint32_t row[32];  // row[b] bit a: bit b of (K * e_a), e_a = the register with only bit a set
+};
+constexpr GfMat cx_mat(uint32_t K) {
+  GfMat m{};
+  for (int a = 0; a < 32; ++a) {
+    const uint32_t c = cx_mult(K, 1u << a);
+    for (int b = 0; b < 32; ++b)
+      if ((c >> b) & 1u) m.row[b] |= 1u << a;
+  }
+  return m;
+}
+
+// in[a] for every set bit a of the compile-time mask M, XOR-ed into acc, two
+// terms per 3-input XOR (v_bitop3_b32; the transpose's selects are inline asm:
+// LLVM otherwise re-associates this XOR network through them and multiplies
+// its size by six)
+template <uint32_t M, int A = 0>
+__device__ __forceinline__ uint32_t xor_terms(const uint32_t (&in)[32], uint32_t acc) {
+  if constexpr (A == 32) {
+    return acc;
+  } else if constexpr (((M >> A) & 1u) == 0) {
+    return xor_terms<M, A + 1>(in, acc);
+  } else {
+    constexpr uint32_t rest = M & ~((2u << A) - 1u);  // set bits above A
+    if constexpr (rest == 0) {
+      return acc ^ in[A];
+    } else {
+      constexpr int A2 = __builtin_ctz(rest);
+      return xor_terms<M, A2 + 1>(in, __builtin_amdgcn_bitop3_b32(acc, in[A], in[A2], 0x96));
+    }
+  }
+}
+template <uint32_t K, int B = 0>
+__device__ __forceinline__ void gf_rows(const uint32_t (&in)[32], const uint32_t (&add)[32], uint32_t (&out)[32]) {
+  if constexpr (B < 32) {
+    constexpr uint32_t M = cx_mat(K).row[B];
+    out[B] = xor_terms<M>(in, add[B]);
+    gf_rows<K, B + 1>(in, add, out);
+  }
+}
+// out[b] = add[b] ^ (K * stream) bit b: the 32 streams of the planes each
+// multiplied by K
+template <uint32_t K>
+__device__ __forceinline__ void gf_mul_planes(const uint32_t (&in)[32], const uint32_t (&add)[32], uint32_t (&out)[32]) {
+  gf_rows<K>(in, add, out);
+}
+
+// 32 x 32 bit transpose in place: afterwards w[b] bit j = bit b of the
+// former w[j].  Block swaps of 16 and 8 bits by byte permutes, 4, 2, 1 by
+// shifts and bit-field selects (v_bfi_b32).
+// (builtins, not inline asm: the hazard recognizer then knows them and adds
+// no s_nop between dependent ones)
+__device__ __forceinline__ uint32_t perm_asm(uint32_t s0, uint32_t s1, uint32_t sel) {
+  return __builtin_amdgcn_perm(s0, s1, sel);
+}
+__device__ __forceinline__ uint32_t bfi_asm(uint32_t m, uint32_t a, uint32_t b) {  // (m & a) | (~m & b)
+  return __builtin_amdgcn_bitop3_b32(m, a, b, 0xCA);
+}
+// rows k and k + S (k & S == 0): bits of the S-wide columns exchanged
+template <int S>
+__device__ __forceinline__ void swap_stage(uint32_t (&w)[32], uint32_t m) {
+#pragma unroll
+  for (int k = 0; k < 32; ++k) {
+    if ((k & S) == 0) {
+      const uint32_t a = w[k], b = w[k + S];
+      w[k] = bfi_asm(m, a, b << S);
+      w[k + S] = bfi_asm(m, a >> S, b);
+    }
+  }
+}
+__device__ __forceinline__ void transpose32(uint32_t (&w)[32]) {
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const uint32_t a = w[k], b = w[k + 16];
+    w[k] = perm_asm(b, a, 0x05040100u);       // a.lo16 | b.lo16 << 16
+    w[k + 16] = perm_asm(b, a, 0x07060302u);  // a.hi16 | b.hi16 << 16
+  }
+#pragma unroll
+  for (int k0 = 0; k0 < 32; k0 += 16)
+#pragma unroll
+    for (int k = k0; k < k0 + 8; ++k) {
+      const uint32_t a = w[k], b = w[k + 8];
+      w[k] = perm_asm(b, a, 0x06020400u);      // bytes a0 b0 a2 b2
+      w[k + 8] = perm_asm(b, a, 0x07030501u);  // bytes a1 b1 a3 b3
+    }
+  swap_stage<4>(w, 0x0F0F0F0Fu);
+  swap_stage<2>(w, 0x33333333u);
+  swap_stage<1>(w, 0x55555555u);
 }
 
 __device__ __forceinline__ uint32_t crc_byte(uint32_t c, uint32_t b) {
@@ -159,7 +259,7 @@ __device__ inline uint32_t shift_bytes(const uint32_t *__restrict__ dig, const u
 }
 
 template <bool DO_CRC, bool DO_ADLER>
-__global__ __launch_bounds__(CK_THREADS) void checksum_segments(const uint8_t *__restrict__ frame0, size_t lo0,
+__global__ __launch_bounds__(CK_THREADS, ZT_CK_MINW) void checksum_segments(const uint8_t *__restrict__ frame0, size_t lo0,
                                                                  size_t hi0, size_t nseg,
                                                                  const uint32_t *__restrict__ nib_g,
                                                                  const uint32_t *__restrict__ x2n_g,
@@ -167,7 +267,7 @@ __global__ __launch_bounds__(CK_THREADS) void checksum_segments(const uint8_t *_
                                                                  SegResult *__restrict__ out,
                                                                  const CkJob *__restrict__ jobs = nullptr) {
   // 32 KiB of replicated nibble tables + the combine scratch
-  __shared__ uint32_t T[DO_CRC ? NIB_ENTRIES * 32 : 1];
+  __shared__ uint32_t T[DO_CRC ? 256 * 32 : 1];  // nibble positions 0..15 (ragged slices only)
   __shared__ uint32_t x2n[32];
   __shared__ uint32_t red_c[1];
   __shared__ unsigned long long red_a[CK_THREADS / 64][2];
@@ -178,11 +278,11 @@ __global__ __launch_bounds__(CK_THREADS) void checksum_segments(const uint8_t *_
   if (DO_CRC) {
     // all loads in flight before the LDS stores (one call's latency matters
     // for small inputs)
-    uint32_t tv[NIB_ENTRIES * 32 / CK_THREADS];
+    uint32_t tv[256 * 32 / CK_THREADS];
 #pragma unroll
-    for (int k = 0; k < NIB_ENTRIES * 32 / CK_THREADS; ++k) tv[k] = nib_g[nib_index(tid + k * CK_THREADS)];
+    for (int k = 0; k < 256 * 32 / CK_THREADS; ++k) tv[k] = nib_g[nib_index(tid + k * CK_THREADS)];
 #pragma unroll
-    for (int k = 0; k < NIB_ENTRIES * 32 / CK_THREADS; ++k) T[tid + k * CK_THREADS] = tv[k];
+    for (int k = 0; k < 256 * 32 / CK_THREADS; ++k) T[tid + k * CK_THREADS] = tv[k];
     if (tid < 32) x2n[tid] = x2n_g[tid];
   }
   __syncthreads();
@@ -206,68 +306,95 @@ __global__ __launch_bounds__(CK_THREADS) void checksum_segments(const uint8_t *_
     const bool whole = seg_lo >= lo && seg_lo + CK_SEG <= hi;
     uint64_t a1 = 0, a2 = 0;  // Adler sums of this thread's bytes, positions weighted to the segment end
     if (whole) {
-      // coalesced lane stream: wave w's 64 KiB in rows of CK_RB bytes, lane
-      // l's piece of row k the CK_P bytes at CK_RB k + CK_P l (CK_Q loads of
-      // 16 bytes); the lane's CRC advances once per row, so its lookups per
-      // byte are 2 + 0.5 / CK_Q
+      // wave w's bytes in rows of 8 KiB; lane l's 16-byte piece q of row r
+      // at 8192 r + 1024 q + 16 l: stream j = 4 q + w of the lane is word w
+      // of piece q of every row (bit-sliced CRC, see the header)
       const int wv = tid >> 6, ln = tid & 63;
-      const uint4 *p = reinterpret_cast<const uint4 *>(frame + seg_lo + (size_t)wv * CK_WAVE_BYTES) + ln * CK_Q;
-      uint32_t L = 0, S = 0, KS = 0, JS = 0, W = 0;
-      constexpr int ROWS = CK_WAVE_BYTES / CK_RB, B = ZT_CK_B;
-      constexpr int RQ = CK_RB / 16;  // uint4 per row
-      uint4 v[B * CK_Q], nx[B * CK_Q];
+      const uint4 *p = reinterpret_cast<const uint4 *>(frame + seg_lo + (size_t)wv * CK_WAVE_BYTES) + ln;
+      constexpr int RQ = CK_ROW / 16;  // uint4 per row
+      uint32_t P[32];
 #pragma unroll
-      for (int k = 0; k < B; ++k)
+      for (int b = 0; b < 32; ++b) P[b] = 0;
+      uint32_t S = 0, KS = 0, QS = 0, W = 0;
+      uint4 v[8], nx[8];
 #pragma unroll
-        for (int j = 0; j < CK_Q; ++j) v[k * CK_Q + j] = ld_stream(p + k * RQ + j);
+      for (int q = 0; q < 8; ++q) v[q] = ld_stream(p + q * 64);
+      // one row: Adler sums of its 8 pieces, the CRC streams one row on
+      auto row = [&](const uint4 (&x8)[8], int r, const uint32_t (&pin)[32], uint32_t (&pout)[32]) {
+        if (DO_ADLER) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const uint4 x = x8[q];
+            uint32_t wsum = __builtin_amdgcn_udot4(x.x, 0x0D0E0F10u, 0u, false);
+            wsum = __builtin_amdgcn_udot4(x.y, 0x090A0B0Cu, wsum, false);
+            wsum = __builtin_amdgcn_udot4(x.z, 0x05060708u, wsum, false);
+            wsum = __builtin_amdgcn_udot4(x.w, 0x01020304u, wsum, false);
+            uint32_t sk = __builtin_amdgcn_udot4(x.x, 0x01010101u, 0u, false);
+            sk = __builtin_amdgcn_udot4(x.y, 0x01010101u, sk, false);
+            sk = __builtin_amdgcn_udot4(x.z, 0x01010101u, sk, false);
+            sk = __builtin_amdgcn_udot4(x.w, 0x01010101u, sk, false);
+            S += sk;
+            KS += (uint32_t)r * sk;
+            QS += (uint32_t)q * sk;
+            W += wsum;
+          }
+        }
+        if (DO_CRC) {
+          uint32_t d[32];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            d[4 * q] = x8[q].x;
+            d[4 * q + 1] = x8[q].y;
+            d[4 * q + 2] = x8[q].z;
+            d[4 * q + 3] = x8[q].w;
+          }
+          transpose32(d);
+          gf_mul_planes<cx_x8n(CK_ROW)>(pin, d, pout);  // every stream: one row on
+        }
+      };
+      static_assert(CK_ROWS % 2 == 0, "rows go in pairs");
+      uint32_t Q[32];
 #pragma unroll 1
-      for (int r0 = 0; r0 < ROWS; r0 += B) {
-        if (r0 + B < ROWS) {
+      for (int r = 0; r < CK_ROWS; r += 2) {
+        // rows r (v) and r + 1 (nx): registers ping-pong, no copies
 #pragma unroll
-          for (int k = 0; k < B; ++k)
+        for (int q = 0; q < 8; ++q) nx[q] = ld_stream(p + (r + 1) * RQ + q * 64);
+        row(v, r, P, Q);
+        if (r + 2 < CK_ROWS) {
 #pragma unroll
-            for (int j = 0; j < CK_Q; ++j) nx[k * CK_Q + j] = ld_stream(p + (r0 + B + k) * RQ + j);
+          for (int q = 0; q < 8; ++q) v[q] = ld_stream(p + (r + 2) * RQ + q * 64);
         }
-#pragma unroll
-        for (int k = 0; k < B; ++k) {
-          if (DO_CRC) {
-            uint32_t r = 0;  // raw CRC of the lane's piece
-#pragma unroll
-            for (int j = 0; j < CK_Q; ++j) {
-              const uint4 x = v[k * CK_Q + j];
-              r = crc_step8(crc_step8(r, x.x, x.y, T, lane32), x.z, x.w, T, lane32);
-            }
-            L = crc_adv1k(L, r, T, lane32);
-          }
-          if (DO_ADLER) {
-#pragma unroll
-            for (int j = 0; j < CK_Q; ++j) {
-              const uint4 x = v[k * CK_Q + j];
-              uint32_t wsum = __builtin_amdgcn_udot4(x.x, 0x0D0E0F10u, 0u, false);
-              wsum = __builtin_amdgcn_udot4(x.y, 0x090A0B0Cu, wsum, false);
-              wsum = __builtin_amdgcn_udot4(x.z, 0x05060708u, wsum, false);
-              wsum = __builtin_amdgcn_udot4(x.w, 0x01020304u, wsum, false);
-              uint32_t sk = __builtin_amdgcn_udot4(x.x, 0x01010101u, 0u, false);
-              sk = __builtin_amdgcn_udot4(x.y, 0x01010101u, sk, false);
-              sk = __builtin_amdgcn_udot4(x.z, 0x01010101u, sk, false);
-              sk = __builtin_amdgcn_udot4(x.w, 0x01010101u, sk, false);
-              S += sk;
-              KS += (uint32_t)(r0 + k) * sk;
-              JS += (uint32_t)j * sk;
-              W += wsum;
-            }
-          }
-        }
-#pragma unroll
-        for (int k = 0; k < B * CK_Q; ++k) v[k] = nx[k];
+        row(nx, r + 1, Q, P);
       }
-      c = L;
+      if (DO_CRC) {
+        // (the planes are pinned here: LLVM otherwise moves the folds below
+        // into the row loop and runs them, selected away, on every row)
+#pragma unroll
+        for (int b = 0; b < 32; ++b) asm volatile("" : "+v"(P[b]));
+        // fold the streams: j and j + h, whose words are D_h bytes apart, into j
+        uint32_t t[32], u[32];
+#define CK_FOLD(H, D)                                                   \
+  {                                                                     \
+    _Pragma("unroll") for (int b = 0; b < 32; ++b) t[b] = P[b] >> (H);  \
+    gf_mul_planes<cx_x8n(D)>(P, t, u);                                  \
+    _Pragma("unroll") for (int b = 0; b < 32; ++b) P[b] = u[b];         \
+  }
+        CK_FOLD(16, 4096)
+        CK_FOLD(8, 2048)
+        CK_FOLD(4, 1024)
+        CK_FOLD(2, 8)
+        CK_FOLD(1, 4)
+#undef CK_FOLD
+        uint32_t y = 0;
+#pragma unroll
+        for (int b = 0; b < 32; ++b) y |= (P[b] & 1u) << b;
+        c = y;  // the lane's register before its last word's 32 bit steps (folded into its shift)
+      }
       len = CK_SLICE;
-      // byte b of load j of row k sits CK_SEG - (64 KiB w + CK_RB k + CK_P l + 16 j + b)
-      // bytes before the segment end
-      const uint64_t cw = (uint64_t)CK_SEG - (uint64_t)wv * CK_WAVE_BYTES - (uint64_t)CK_P * (uint32_t)ln - 16u;
+      // byte k of piece q of row r sits CK_SEG - (wave_off + 8192 r + 1024 q + 16 l + k) bytes before the segment end
+      const uint64_t cw = (uint64_t)CK_SEG - (uint64_t)wv * CK_WAVE_BYTES - 16ull * (uint32_t)ln - 16u;
       a1 = S;
-      a2 = cw * S - (uint64_t)CK_RB * KS - 16ull * JS + W;
+      a2 = cw * S - (uint64_t)CK_ROW * KS - 1024ull * QS + W;
     } else if (v_lo == s_lo && v_hi == s_lo + CK_SLICE) {
       len = CK_SLICE;
       const uint4 *p = reinterpret_cast<const uint4 *>(frame + s_lo);
@@ -486,19 +613,19 @@ void crc_host_tables(uint32_t byte_table[256], uint32_t nib[ZT_CRC_NIB_N], uint3
   }
   x2n[0] = 1u << 30;  // x^1
   for (int k = 1; k < 32; ++k) x2n[k] = multmodp(x2n[k - 1], x2n[k - 1]);
-  // nib[(ADV + j) * 16 + v]: (v << 4 j) * x^(8 * CK_RB) mod P
-  const uint32_t k1 = x2nmodp(x2n, CK_RB, 3);
-  for (int j = 0; j < 8; ++j)
-    for (uint32_t v = 0; v < 16; ++v) nib[(ADV + j) * 16 + v] = multmodp(k1, v << (4 * j));
+  // (entries [256, 384) unused: the whole-segment path is table-free)
+  for (int i = 256; i < ZT_CRC_NIB_N; ++i) nib[i] = 0;
 }
 
 void crc_shift_tables(const uint32_t x2n[32], uint32_t shift[ZT_CRC_SHIFT_N]) {
-  // lane streams of a whole segment: thread t = 64 w + l ends CK_P bytes past
-  // W w + W - CK_RB + CK_P l (W = CK_WAVE_BYTES), i.e. W (waves - 1 - w) +
-  // CK_RB - CK_P (l + 1) before the segment end
+  // lanes of a whole segment: thread t = 64 w + l holds y with its CRC
+  // register = y * x^32, ending CK_WAVE_BYTES (waves - 1 - w) + 1024 - 16 (l +
+  // 1) bytes before the segment end (bit-sliced path, checksum_segments):
+  // the shift x^(8 after + 32)
   for (int t = 0; t < CK_THREADS; ++t) {
-    const uint64_t after = (uint64_t)CK_WAVE_BYTES * (CK_THREADS / 64 - 1 - t / 64) + CK_RB - CK_P * (t % 64 + 1);
-    shift[ZT_CRC_LANE_OFF + t] = x2nmodp(x2n, after, 3);
+    const uint64_t after =
+        (uint64_t)CK_WAVE_BYTES * (CK_THREADS / 64 - 1 - t / 64) + 1024 - 16 * (uint64_t)(t % 64 + 1);
+    shift[ZT_CRC_LANE_OFF + t] = x2nmodp(x2n, after + 4, 3);
   }
   // digit tables: x^(8 * v * 64^d)
   for (int d = 0; d < ZT_CRC_DIGITS; ++d)

@@ -58,6 +58,19 @@ __device__ unsigned long long g_df_count[4];  // debug: pair steps (per wave), l
 #define ZT_DF_BLOCK 32768
 #endif
 constexpr int DF_BLOCK = ZT_DF_BLOCK;
+// DEFLATE blocks (one Huffman code, one header, one sync point) may span
+// DF_GROUP consecutive 32 KiB parse blocks of a stream (compile option): the
+// match / price / DP / parse kernels keep their 32 KiB granularity,
+// block_kernel sums the group's histograms and encode_kernel writes the
+// group's tokens as one block.  Inflate units are one DEFLATE block
+// (inflate_seg.hip).  Measured at 4 (profiles/r03b_*): wordsalad ratio vs the
+// reference 1.0168 -> 1.0145 only, but inflate 10.9 -> 12.2 ms per GiB
+// (tokenize and expand get a quarter of the units): kept at 1.
+#ifndef ZT_DF_GROUP
+#define ZT_DF_GROUP 1
+#endif
+constexpr int DF_GROUP = ZT_DF_GROUP;
+static_assert(DF_GROUP >= 1 && DF_GROUP <= 8 && (32 % DF_GROUP) == 0, "group divides a segment");
 constexpr int DF_SUB = 4096;
 constexpr int DF_RING = 32768;  // power of two: ring index = rel & (DF_RING - 1)
 constexpr int DF_SLOT = DF_BLOCK + DF_BLOCK / 8 + 1024;  // per-block slot: fits a forced fixed-code block
@@ -125,13 +138,15 @@ struct DeflateParams {
 struct BlockPlan {
   uint32_t lit_code[288];  // len << 16 | bit-reversed code
   uint32_t dist_code[32];
-  uint32_t ntok;
+  uint32_t ntok;      // tokens of the group
   uint32_t btype;     // 0 stored, 1 fixed, 2 dynamic
   uint32_t hdr_bits;  // header bits (complete words already in the slot)
   uint32_t hdr_tail;  // bits [hdr_bits & ~31, hdr_bits) of the header, not yet stored
-  uint32_t blen;
+  uint32_t blen;      // input bytes of the group
   uint32_t last;
-  uint32_t pad[2];
+  uint32_t nsub;      // parse blocks in the group (<= DF_GROUP)
+  uint32_t pad;
+  uint32_t ntok_sub[8];  // tokens per parse block (in res at (leader + k) * DF_BLOCK)
 };
 
 namespace {
@@ -139,6 +154,19 @@ namespace {
 // end of the stream block `blk` belongs to (relative to base + halo)
 __device__ __forceinline__ uint64_t stream_end(const DeflateParams &P, uint32_t blk) {
   return P.span ? P.span[2 * (uint64_t)blk + 1] : P.end - P.halo;
+}
+
+// a DEFLATE block (group) starts at every DF_GROUP-th parse block of its
+// stream (batch: counted from the stream's first block)
+__device__ __forceinline__ bool group_leader(const DeflateParams &P, uint32_t blk) {
+  const uint64_t first = P.span ? P.span[2 * (uint64_t)blk] / DF_BLOCK : 0;
+  return ((blk - first) % DF_GROUP) == 0;
+}
+// parse blocks in the group led by `blk`
+__device__ __forceinline__ uint32_t group_size(const DeflateParams &P, uint32_t blk) {
+  const uint64_t lo = (uint64_t)blk * DF_BLOCK, n = stream_end(P, blk);
+  const uint64_t nb = (n - lo + DF_BLOCK - 1) / DF_BLOCK;
+  return nb < (uint64_t)DF_GROUP ? (uint32_t)nb : (uint32_t)DF_GROUP;
 }
 
 __constant__ uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
@@ -1390,21 +1418,32 @@ __global__ __launch_bounds__(64) void parse_kernel(DeflateParams P) {
   if (lane == 0) hs[320] = ntok;
 }
 
+// one wave per DEFLATE block: launched per parse block, the group's leader
+// works, the others return
 __global__ __launch_bounds__(64) void block_kernel(DeflateParams P) {
   __shared__ BlockShared sh;
   BlockShared *s = &sh;
   const int lane = threadIdx.x;
   const uint32_t blk = blockIdx.x;
+  if (!group_leader(P, blk)) return;
+  const uint32_t nsub = group_size(P, blk);
   const uint64_t lo = (uint64_t)blk * DF_BLOCK;
   const uint64_t n = stream_end(P, blk);
-  const uint32_t blen = (uint32_t)((n - lo) < DF_BLOCK ? (n - lo) : DF_BLOCK);
+  const uint64_t gspan = (uint64_t)nsub * DF_BLOCK;
+  const uint32_t blen = (uint32_t)((n - lo) < gspan ? (n - lo) : gspan);
   BlockPlan *plan = P.plans + blk;
-  const bool last = P.span ? lo + DF_BLOCK >= n : P.final_ && (blk == P.nblocks - 1);
-  // the parse's histograms and token count (parse_kernel, in the block's slot)
-  const uint32_t *hs = reinterpret_cast<const uint32_t *>(P.slots + (size_t)blk * DF_SLOT);
-  for (int i = lane; i < 288; i += 64) s->lit_hist[i] = hs[i];
-  if (lane < 32) s->dist_hist[lane] = hs[288 + lane];
-  const uint32_t ntok = hs[320];
+  const bool last = P.span ? lo + gspan >= n : P.final_ && (blk + nsub == P.nblocks);
+  // the parse's histograms and token counts (parse_kernel, in each parse
+  // block's slot), summed over the group
+  uint32_t ntok = 0;
+  for (uint32_t k = 0; k < nsub; ++k) {
+    const uint32_t *hs = reinterpret_cast<const uint32_t *>(P.slots + (size_t)(blk + k) * DF_SLOT);
+    for (int i = lane; i < 288; i += 64) s->lit_hist[i] = (k ? s->lit_hist[i] : 0u) + hs[i];
+    if (lane < 32) s->dist_hist[lane] = (k ? s->dist_hist[lane] : 0u) + hs[288 + lane];
+    const uint32_t nt = hs[320];
+    if (lane == 0) plan->ntok_sub[k] = nt;
+    ntok += nt;
+  }
   wsync();
 #ifdef ZT_DF_TIME
   uint64_t bt0 = __builtin_readcyclecounter(), btk;
@@ -1633,6 +1672,7 @@ __global__ __launch_bounds__(64) void block_kernel(DeflateParams P) {
     plan->hdr_tail = htail;
     plan->blen = blen;
     plan->last = last ? 1 : 0;
+    plan->nsub = nsub;
   }
   BK_T(5);
 #ifdef ZT_DF_TIME
@@ -1741,15 +1781,33 @@ __device__ __forceinline__ void for_tokens(const uint32_t *tok, uint32_t a, uint
   for (; i < b; ++i) f(tok[i]);
 }
 
+// f(token) for tokens [a, b) of the group's concatenated token lists
+template <typename F>
+__device__ __forceinline__ void for_group_tokens(const DeflateParams &P, const BlockPlan *plan, uint32_t blk,
+                                                 uint32_t a, uint32_t b, F &&f) {
+  uint32_t off = 0;
+  for (uint32_t k = 0; k < plan->nsub && off < b; ++k) {
+    const uint32_t nk = plan->ntok_sub[k];
+    const uint32_t lo = a > off ? a - off : 0u, hi = b - off < nk ? b - off : nk;
+    if (lo < hi) for_tokens(P.res + (uint64_t)(blk + k) * DF_BLOCK, lo, hi, f);
+    off += nk;
+  }
+}
+
+// one workgroup per DEFLATE block (launched per parse block; followers
+// return): the group's stream goes to the leader's slot and on into the
+// followers' (contiguous, DF_SLOT each), whose lengths are 0
 __global__ __launch_bounds__(ENC_THREADS) void encode_kernel(DeflateParams P) {
   __shared__ EncShared sh;
   EncShared *s = &sh;
   const uint32_t t = threadIdx.x;
   const uint32_t blk = blockIdx.x;
+  if (!group_leader(P, blk)) return;
   const BlockPlan *plan = P.plans + blk;
   const uint32_t bt = plan->btype, blen = plan->blen;
   const bool last = plan->last != 0;
   uint8_t *slot_bytes = P.slots + (size_t)blk * DF_SLOT;
+  if (t > 0 && t < plan->nsub) P.slot_len[blk + t] = 0;
   if (bt == 0) {
     // stored block: header byte, LEN, NLEN, data
     const uint8_t *raw = P.base + P.halo + (uint64_t)blk * DF_BLOCK;
@@ -1783,11 +1841,14 @@ __global__ __launch_bounds__(ENC_THREADS) void encode_kernel(DeflateParams P) {
   __syncthreads();
   const uint32_t ntok = plan->ntok;
   const uint32_t hdr_bits = plan->hdr_bits;
-  const uint32_t *tok = P.res + (uint64_t)blk * DF_BLOCK;
   const uint32_t a = (uint32_t)(((uint64_t)ntok * t) / ENC_THREADS);
   const uint32_t b = (uint32_t)(((uint64_t)ntok * (t + 1)) / ENC_THREADS);
   uint32_t bits = 0;
-  for_tokens(tok, a, b, [&](uint32_t tk) { bits += token_bits(s, tk); });
+  const uint32_t *tok = P.res + (uint64_t)blk * DF_BLOCK;  // (DF_GROUP 1: the block's own tokens)
+  if constexpr (DF_GROUP == 1)
+    for_tokens(tok, a, b, [&](uint32_t tk) { bits += token_bits(s, tk); });
+  else
+    for_group_tokens(P, plan, blk, a, b, [&](uint32_t tk) { bits += token_bits(s, tk); });
   if (t == 0) bits += hdr_bits;
   const uint32_t eob = s->lit_code[256] >> 16;
   if (t == ENC_THREADS - 1) bits += eob;  // marker bits appended after the scan
@@ -1822,7 +1883,10 @@ __global__ __launch_bounds__(ENC_THREADS) void encode_kernel(DeflateParams P) {
     bo.acc = plan->hdr_tail;
     bo.first_partial = false;  // nothing left of thread 0 shares its first word
   }
-  for_tokens(tok, a, b, [&](uint32_t tk) { put_token(bo, s, tk); });
+  if constexpr (DF_GROUP == 1)
+    for_tokens(tok, a, b, [&](uint32_t tk) { put_token(bo, s, tk); });
+  else
+    for_group_tokens(P, plan, blk, a, b, [&](uint32_t tk) { put_token(bo, s, tk); });
   if (t == ENC_THREADS - 1) {
     const uint32_t c = s->lit_code[256];
     bo.put(c & 0xFFFF, c >> 16);

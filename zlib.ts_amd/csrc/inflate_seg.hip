@@ -53,7 +53,12 @@ bool inf_debug() {
 #ifndef ZT_DF_BLOCK
 #define ZT_DF_BLOCK 32768
 #endif
-constexpr uint32_t kUnitTokCap = ZT_DF_BLOCK + 64;  // this engine's units are one block: <= 1 token per byte
+#ifndef ZT_DF_GROUP
+#define ZT_DF_GROUP 1
+#endif
+// this engine's units are one DEFLATE block of ZT_DF_GROUP parse blocks
+// (deflate.hip): <= 1 token per byte
+constexpr uint32_t kUnitTokCap = ZT_DF_BLOCK * ZT_DF_GROUP + 64;
 
 // sync point = byte after an aligned 00 00 FF FF; list entry = pos << 1 | restart
 // One 16-byte aligned chunk per lane, loaded as one 16-byte word; the 8 bytes
@@ -232,7 +237,12 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   // than its decode needs: past a budget tied to the input size, or when the
   // slots cannot be allocated, the stream takes the one-wave path instead.
   const size_t tok_bytes = (units * (size_t)kUnitTokCap + 256) * 4;  // + slack: chunked token reads
-  if (tok_bytes > 16 * (n - index) + (64u << 20)) FALLBACK("%zu sync candidates: token slots over budget\n", units);
+  // (a highly compressible stream needs far more token bytes than its own
+  // size -- ~4 bytes per output byte -- so the budget is the device's free
+  // memory, not a multiple of the input)
+  size_t mem_free = 0, mem_total = 0;
+  ZT_HIP(hipMemGetInfo(&mem_free, &mem_total));
+  if (tok_bytes > c->buf_size[4] + mem_free / 2) FALLBACK("%zu sync candidates: token slots over budget\n", units);
   void *d_tok;
   if (scratch(c, 4, tok_bytes, &d_tok) != ZT_OK) FALLBACK("token slots (%zu B) not allocated\n", tok_bytes);
   // metadata comes back through pinned staging (slot 1):
