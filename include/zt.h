@@ -274,9 +274,13 @@ typedef struct zt_inflate_plan zt_inflate_plan;
 int zt_inflate_plan_create(size_t max_in, size_t max_out, zt_inflate_plan **plan);
 void zt_inflate_plan_destroy(zt_inflate_plan *plan);
 /* Inflate the raw stream d_in[0..n) into d_out (capacity out_cap).  Streams
- * carrying restart points (two empty stored blocks, which zt_deflate_dev
- * writes every 1 MiB of input) are decoded segment-parallel; others by one
- * wavefront.  Results are identical either way. */
+ * carrying sync / restart points (empty stored blocks, which zt_deflate_dev
+ * writes after every block and every 1 MiB of input) are decoded
+ * segment-parallel (inflate_seg.hip + inflate_tok.hip); any other stream --
+ * the reference's own single-block output, zlib / gzip streams -- by the
+ * general speculative decoder (inflate_gen.hip); a stream neither path
+ * finishes (a corrupt one) by one wavefront, which reports the reference's
+ * exact error.  Results are identical whichever path decodes. */
 int zt_inflate_dev(zt_inflate_plan *plan, const void *d_in, size_t n, void *d_out, size_t out_cap,
                    size_t *out_len, size_t *end_ip, void *stream);
 

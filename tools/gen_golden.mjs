@@ -8,7 +8,10 @@
 // differently-cased name).  Refuses to run when /root/reference is absent
 // (e.g. on the GPU box): the committed fixtures are what travels.
 //
-//   node tools/gen_golden.mjs [outdir]
+//   node --max-old-space-size=16384 tools/gen_golden.mjs [outdir]
+//
+// (the 1 GiB checksum pins and the large inflate cases need the bigger heap:
+// Node 12's default heap aborts with an out-of-memory error)
 //
 // Input generators are restated in tests/gen.py; each fixture records the
 // generator spec so Python can rebuild large inputs instead of storing them.
