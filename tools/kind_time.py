@@ -1,7 +1,7 @@
 # Per-generator cost of the bench pipeline: 256 MiB of one generator (device
 # synthetic corpus) deflated and inflated through the device plans,
 # kernel intervals from the library's HIP-event timers (ms per 256 MiB), and the
-# ratio.   usage: python tools/kind_time.py [MiB]
+# ratio.   usage: python tools/kind_time.py [MiB] [generator...]
 import os
 import sys
 
@@ -16,7 +16,7 @@ d_c = torch.empty(zt.deflate_bound(n) + 64, dtype=torch.uint8, device="cuda")
 d_out = torch.empty(n + 4096, dtype=torch.uint8, device="cuda")
 dp = zt.DeflatePlan(n, level=6)
 ip = zt.InflatePlan(zt.deflate_bound(n) + 64, n)
-for kind in ["wordsalad", "xorshift32", "structured"]:
+for kind in sys.argv[2:] or ["wordsalad", "xorshift32", "structured"]:
     zt.synth_dev(kind, 11, d_in.data_ptr(), n)
     clen = dp.run(d_in.data_ptr(), n, d_c.data_ptr())
     ip.run(d_c.data_ptr(), clen, d_out.data_ptr(), d_out.numel())

@@ -275,6 +275,7 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   }
   tp.dump_unit = getenv("ZT_TOK_DUMP") ? (uint32_t)atoi(getenv("ZT_TOK_DUMP")) : 0xFFFFFFFFu;
   tp.dump_once = 0;
+  ZT_TRY(tok_runs_setup(c, tp, n, s));
   ZT_TRY(timing_begin(c, s, 3));
   ZT_TRY(tokenize_units_dev(tp, s));
   ZT_TRY(timing_end(c, s, 3));

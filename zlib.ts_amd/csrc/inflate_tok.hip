@@ -39,11 +39,12 @@ struct TokShared {
 };
 
 
-#ifdef ZT_TOK_WAVES
-#define ZT_TOK_ATTR __attribute__((amdgpu_waves_per_eu(ZT_TOK_WAVES)))
-#else
-#define ZT_TOK_ATTR
+// 3 waves per SIMD: the register budget (<= 168 VGPRs) the body decoder
+// fits in; the compiler's own choice drifts to 169+ (2 waves) on small edits
+#ifndef ZT_TOK_WAVES
+#define ZT_TOK_WAVES 3
 #endif
+#define ZT_TOK_ATTR __attribute__((amdgpu_waves_per_eu(ZT_TOK_WAVES)))
 __global__ __launch_bounds__(64) ZT_TOK_ATTR void tokenize_kernel(TokParams P) {
   __shared__ TokShared sh;
   __shared__ SpecShared spsh;
@@ -92,7 +93,24 @@ __global__ __launch_bounds__(64) ZT_TOK_ATTR void tokenize_kernel(TokParams P) {
       }
       if (len) {
         to.flush_partial();
-        for (uint32_t j = lane; j < len; j += 64) to.tok[nt0 + j] = gin[p + j];
+        // a long payload is handed to stored_fill_kernel (wide copies after
+        // this kernel); every lane takes part in the claim (no lane-0 branch
+        // inside the block loop), lane 0 adding the one
+        bool inline_copy = true;
+        if (P.runs && len >= kStoredRunMin) {
+          const uint32_t k = uni(atomicAdd(P.nruns, lane == 0 ? 1u : 0u));
+          if (k < P.runs_cap) {
+            inline_copy = false;
+            StoredRun r;  // (every lane stores the same record)
+            r.src = p;
+            r.dst = (uint64_t)(to.tok - P.tokens) + nt0;
+            r.len = len;
+            r.pad = 0;
+            P.runs[k] = r;
+          }
+        }
+        if (inline_copy)
+          for (uint32_t j = lane; j < len; j += 64) to.tok[nt0 + j] = gin[p + j];
         const uint32_t nt = nt0 + len;
         const uint32_t idx = (nt & ~63u) + (uint32_t)lane;
         if ((uint32_t)lane < (nt & 63) && idx >= nt0) to.stg = gin[p + idx - nt0];
@@ -462,12 +480,51 @@ __global__ __launch_bounds__(64) void copy_kernel(ResolveParams P) {
   if (lane == 0) P.seg_status[sg] = ZT_OK;
 }
 
+// stored payloads -> literal tokens: one run per workgroup (grid-stride),
+// 8 byte loads per thread in flight (HBM: 1 byte read + 4 written per byte)
+constexpr int kFillGrid = 2048;
+__global__ __launch_bounds__(256) void stored_fill_kernel(const uint8_t *__restrict__ in,
+                                                          const StoredRun *__restrict__ runs,
+                                                          const uint32_t *__restrict__ nruns, uint32_t cap,
+                                                          uint32_t *__restrict__ tok) {
+  const uint32_t cnt = *nruns < cap ? *nruns : cap;
+  for (uint32_t r = blockIdx.x; r < cnt; r += gridDim.x) {
+    const StoredRun R = runs[r];
+    const uint8_t *src = in + R.src;
+    uint32_t *dst = tok + R.dst;
+    uint32_t i = threadIdx.x;
+    for (; i + 7 * 256 < R.len; i += 8 * 256) {
+      uint32_t b[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) b[k] = src[i + 256 * k];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) dst[i + 256 * k] = b[k];
+    }
+    for (; i < R.len; i += 256) dst[i] = src[i];
+  }
+}
+
 }  // namespace
 
 int tokenize_units_dev(const TokParams &p, hipStream_t s) {
   if (p.count == 0) return ZT_OK;
   tokenize_kernel<<<p.count, 64, 0, s>>>(p);
   ZT_HIP(hipGetLastError());
+  if (p.runs) {
+    stored_fill_kernel<<<kFillGrid, 256, 0, s>>>(p.in, p.runs, p.nruns, p.runs_cap, p.tokens);
+    ZT_HIP(hipGetLastError());
+  }
+  return ZT_OK;
+}
+
+int tok_runs_setup(DeviceCtx *c, TokParams &p, uint64_t n, hipStream_t s) {
+  const uint64_t cap = n / kStoredRunMin + 64;
+  void *buf;
+  ZT_TRY(scratch(c, 21, 256 + cap * sizeof(StoredRun), &buf));
+  p.nruns = static_cast<uint32_t *>(buf);
+  p.runs = reinterpret_cast<StoredRun *>(static_cast<uint8_t *>(buf) + 256);
+  p.runs_cap = (uint32_t)(cap < 0xFFFFFFFFull ? cap : 0xFFFFFFFFull);
+  ZT_HIP(hipMemsetAsync(p.nruns, 0, 4, s));
   return ZT_OK;
 }
 

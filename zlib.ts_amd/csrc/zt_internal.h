@@ -45,9 +45,9 @@ struct DeviceCtx {
   uint32_t *d_crc_x2n = nullptr;    // x^(2^k) mod P, k = 0..31
   uint32_t *d_crc_shift = nullptr;  // checksum.hip merge constants (crc_shift_tables)
   // scratch
-  void *d_buf[21] = {};  // slot 8: checksum segment partials; 10-17: general inflate (inflate_gen.hip);
-                         // 20: segment inflate's sync-point sort (inflate_seg.hip)
-  size_t buf_size[21] = {};
+  void *d_buf[22] = {};  // slot 8: checksum segment partials; 10-17: general inflate (inflate_gen.hip);
+                         // 20: segment inflate's sync-point sort (inflate_seg.hip); 21: stored runs
+  size_t buf_size[22] = {};
   // second stream: checksums run beside the deflate pipeline in the containers
   hipStream_t aux = nullptr;
   hipEvent_t aux_ev = nullptr;
@@ -218,6 +218,14 @@ struct TokResult {
   int32_t detail;
   int32_t stop_idx;   // sync point where the unit stopped, -1 at BFINAL
 };
+// a stored block's payload, copied into its literal tokens by
+// stored_fill_kernel after tokenize_kernel (the tokenizer only reserves them)
+struct StoredRun {
+  uint64_t src;  // input byte offset of the payload
+  uint64_t dst;  // token index of its first byte
+  uint32_t len;
+  uint32_t pad;
+};
 struct TokParams {
   const uint8_t *in;
   uint64_t n;
@@ -231,7 +239,13 @@ struct TokParams {
   uint64_t *dbg;      // debug: per unit 8 words comparing the SIMT and scalar body decodes, or null
   uint32_t dump_unit; // debug: unit whose first SIMT block dumps per-round lane state after dbg[count * 8]
   uint32_t dump_once;
+  StoredRun *runs;    // stored payloads of >= kStoredRunMin bytes (null: the tokenizer copies every one)
+  uint32_t *nruns;    // records claimed (may pass runs_cap: those payloads are copied inline)
+  uint32_t runs_cap;
 };
+constexpr uint32_t kStoredRunMin = 1024;
+// Scratch slot 21 for the stored runs of an n-byte input; sets p.runs / nruns / runs_cap.
+int tok_runs_setup(DeviceCtx *c, TokParams &p, uint64_t n, hipStream_t s);
 // phase B: units of the chain, grouped by segment
 struct ChainUnit {
   uint64_t tok_off;
