@@ -608,20 +608,9 @@ __global__ __launch_bounds__(64) void copy_marker_kernel(ResolveParams P, const 
     *reinterpret_cast<uint64_t *>(&sh.ring[i]) = m;
   }
   wave_sync();
-  const uint64_t nchunks = (n + 127) / 128;
   uint64_t issued = 0, flushed = 0;
   for (uint64_t op = 0; op < n; op += CP_STEP) {
-    const uint64_t need = (op >> 7) + CP_STEP / 128 < nchunks ? (op >> 7) + CP_STEP / 128 : nchunks;
-    const uint64_t want = need + CP_AHEAD < nchunks ? need + CP_AHEAD : nchunks;
-    while (issued < want) {
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint32_t *>(dsrc + issued * 128) + lane,
-                                       &sh.desc[(issued * 128) & (CP_DESC_RING - 1)], 4, 0, 0);
-      ++issued;
-    }
-    if (issued - need >= CP_AHEAD)
-      __builtin_amdgcn_s_waitcnt(cp_vmcnt(CP_AHEAD));
-    else
-      __builtin_amdgcn_s_waitcnt(0x0F70);
+    cp_desc_fetch(dsrc, sh.desc, op, n, issued, lane);
     uint64_t dd[CP_G];
 #pragma unroll
     for (int g = 0; g < CP_G; ++g) {

@@ -589,17 +589,40 @@ constexpr uint32_t RS_FLUSH = 8192;           // output flush granule
 constexpr uint32_t CP_STEP = ZT_CP_STEP;  // copy_kernel bytes per step (a multiple of 256)
 constexpr int CP_G = CP_STEP / 256;       // 4-byte groups per lane per step
 #ifndef ZT_CP_RING
-#define ZT_CP_RING (CP_STEP <= 256 ? 2048 : 4096)
+#define ZT_CP_RING 4096
 #endif
 #ifndef ZT_CP_AHEAD
-#define ZT_CP_AHEAD (CP_STEP <= 256 ? 12 : 24)
+#define ZT_CP_AHEAD 6
 #endif
-constexpr uint32_t CP_DESC_RING = ZT_CP_RING;  // descriptors staged in LDS (chunks of 128)
-constexpr uint32_t CP_AHEAD = ZT_CP_AHEAD;      // chunks in flight ahead of the step
+constexpr uint32_t CP_CHUNK = 512;              // descriptors per LDS-DMA instruction (16 bytes per lane)
+constexpr uint32_t CP_DESC_RING = ZT_CP_RING;  // descriptors staged in LDS
+constexpr uint32_t CP_AHEAD = ZT_CP_AHEAD;      // chunks in flight ahead of the step's
 static_assert(CP_STEP % 256 == 0 && (CP_STEP & (CP_STEP - 1)) == 0, "copy step");
-static_assert((CP_AHEAD + CP_STEP / 128) * 128 <= CP_DESC_RING && CP_AHEAD < 64, "descriptor ring");
+static_assert((CP_AHEAD + (CP_STEP + CP_CHUNK - 1) / CP_CHUNK) * CP_CHUNK <= CP_DESC_RING && CP_AHEAD < 64,
+              "descriptor ring");
 // s_waitcnt vmcnt(v) with lgkmcnt / expcnt left alone (vmcnt bits 3:0 and 15:14)
 constexpr int cp_vmcnt(uint32_t v) { return (int)(0x0F70u | (v & 15u) | ((v >> 4) << 14)); }
+
+// copy kernels: descriptor chunks up to CP_AHEAD past the ones step [op, op +
+// CP_STEP) reads are in flight (one 1 KiB LDS-DMA each, dsrc 1 KiB aligned,
+// its buffer padded by a chunk), and the step's own have landed
+typedef unsigned int cp_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void cp_desc_fetch(const uint16_t *dsrc, uint16_t *ring, uint64_t op, uint64_t n,
+                                              uint64_t &issued, int lane) {
+  const uint64_t nchunks = (n + CP_CHUNK - 1) / CP_CHUNK;
+  const uint64_t need0 = (op + CP_STEP + CP_CHUNK - 1) / CP_CHUNK;
+  const uint64_t need = need0 < nchunks ? need0 : nchunks;
+  const uint64_t want = need + CP_AHEAD < nchunks ? need + CP_AHEAD : nchunks;
+  while (issued < want) {
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const cp_u32x4 *>(dsrc + issued * CP_CHUNK) + lane,
+                                     ring + ((issued * CP_CHUNK) & (CP_DESC_RING - 1)), 16, 0, 0);
+    ++issued;
+  }
+  if (issued - need >= CP_AHEAD)
+    __builtin_amdgcn_s_waitcnt(cp_vmcnt(CP_AHEAD));
+  else
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+}
 
 }  // namespace
 }  // namespace zt

@@ -347,6 +347,7 @@ __global__ __launch_bounds__(64) void expand_kernel(ResolveParams P) {
   if (lane == 0) P.unit_status[u] = any_bad ? ZT_E_INVALID_DISTANCE : (op != cu.out_len ? ZT_E_INPUT_BROKEN : ZT_OK);
 }
 
+
 typedef unsigned int u32x4r __attribute__((ext_vector_type(4)));
 
 
@@ -358,7 +359,16 @@ struct CopyShared {
 // ring bytes [lo, hi) (segment positions) to out + lo
 __device__ __forceinline__ void cp_flush(const CopyShared *sh, uint8_t *out, uint64_t lo, uint64_t hi, int lane) {
   if (lo >= hi) return;
-  if ((((uintptr_t)out + lo) & 15) == 0 && ((hi - lo) & 15) == 0) {
+  if (hi - lo == RS_FLUSH && (((uintptr_t)out + lo) & 15) == 0) {
+    // a whole granule: every ring read in flight before the stores
+    constexpr int K = RS_FLUSH / 1024;
+    u32x4r v[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      v[k] = *reinterpret_cast<const u32x4r *>(&sh->ring[(lo + (uint64_t)lane * 16 + 1024 * k) & RING_MASK]);
+#pragma unroll
+    for (int k = 0; k < K; ++k) *reinterpret_cast<u32x4r *>(out + lo + (uint64_t)lane * 16 + 1024 * k) = v[k];
+  } else if ((((uintptr_t)out + lo) & 15) == 0 && ((hi - lo) & 15) == 0) {
     for (uint64_t p = lo + (uint64_t)lane * 16; p < hi; p += 1024)
       *reinterpret_cast<u32x4r *>(out + p) = *reinterpret_cast<const u32x4r *>(&sh->ring[p & RING_MASK]);
   } else {
@@ -376,8 +386,17 @@ __device__ __forceinline__ uint32_t cp_byte(const CopyShared *sh, uint64_t op, u
   return lit ? (d & 0xFF) : rv;
 }
 
+#ifdef ZT_CP_TIME
+__device__ unsigned long long g_cp_time[8];  // debug: copy_kernel cycles per phase (lane 0 of each wave), [6] steps, [7] waves
+#define CP_T(v) v = __builtin_readcyclecounter()
+#else
+#define CP_T(v) (void)0
+#endif
 __global__ __launch_bounds__(64) void copy_kernel(ResolveParams P) {
   __shared__ CopyShared sh;
+#ifdef ZT_CP_TIME
+  unsigned long long cp_acc[4] = {0, 0, 0, 0}, ct0 = 0, ct1 = 0, ct2 = 0, ct3 = 0, ct4 = 0, nsteps = 0;
+#endif
   const uint32_t sg = blockIdx.x;
   const int lane = threadIdx.x & 63;
   const SegJob sj = P.segs[sg];
@@ -385,33 +404,27 @@ __global__ __launch_bounds__(64) void copy_kernel(ResolveParams P) {
   const ChainUnit lastu = P.units[sj.first + sj.count - 1];
   const uint64_t n = lastu.out_off + lastu.out_len - seg_out;  // segment bytes
   uint8_t *out = P.out + seg_out;
-  const uint16_t *dsrc = P.desc + P.units[sj.first].desc_off;  // 512-aligned
-  // descriptor chunk c = bytes [128 c, 128 c + 128): one DMA of 4 bytes per lane
-  const uint64_t nchunks = (n + 127) / 128;
-  uint64_t issued = 0;
-  uint64_t flushed = 0;
-  for (uint64_t op = 0; op < n; op += CP_STEP) {
-    const uint64_t need = (op >> 7) + CP_STEP / 128 < nchunks ? (op >> 7) + CP_STEP / 128 : nchunks;
-    const uint64_t want = need + CP_AHEAD < nchunks ? need + CP_AHEAD : nchunks;
-    while (issued < want) {
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint32_t *>(dsrc + issued * 128) + lane,
-                                       &sh.desc[(issued * 128) & (CP_DESC_RING - 1)], 4, 0, 0);
-      ++issued;
-    }
-    if (issued - need >= CP_AHEAD)
-      __builtin_amdgcn_s_waitcnt(cp_vmcnt(CP_AHEAD));
-    else
-      __builtin_amdgcn_s_waitcnt(0x0F70);
-    // lane j: bytes op + 256 g + 4 j .. + 3 for each group g (bytes past n
-    // are never flushed); every byte of a step is a literal or a ring byte
-    // before the step, so all descriptor reads, then all ring reads, are
-    // issued before any write
-    uint64_t dd[CP_G];
+  const uint16_t *dsrc = P.desc + P.units[sj.first].desc_off;  // 512-aligned (cp_desc_fetch's chunks)
+  uint64_t issued = 0, flushed = 0;
+  // lane j: bytes op + 256 g + 4 j .. + 3 for each group g (bytes past n are
+  // never flushed).  The next step's descriptors are fetched and read right
+  // after this step's ring writes, so a step starts with its ring reads.
+  uint64_t dd[CP_G];
+  auto read_desc = [&](uint64_t o) {
 #pragma unroll
     for (int g = 0; g < CP_G; ++g) {
-      const uint32_t x = (uint32_t)op + 256u * g + 4 * (uint32_t)lane;  // ring / descriptor index (masked)
+      const uint32_t x = (uint32_t)o + 256u * g + 4 * (uint32_t)lane;  // ring / descriptor index (masked)
       dd[g] = *reinterpret_cast<const uint64_t *>(&sh.desc[x & (CP_DESC_RING - 1)]);
     }
+  };
+  if (n) {
+    cp_desc_fetch(dsrc, sh.desc, 0, n, issued, lane);
+    read_desc(0);
+  }
+  for (uint64_t op = 0; op < n; op += CP_STEP) {
+    CP_T(ct0);
+    // every byte of a step is a literal or a ring byte before the step, so
+    // all ring reads are issued before any write
     uint32_t bw[CP_G];
     bool in_step = false;
 #pragma unroll
@@ -424,6 +437,7 @@ __global__ __launch_bounds__(64) void copy_kernel(ResolveParams P) {
       bw[g] = b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
       in_step = in_step || o0 >= 0 || o1 >= 0 || o2 >= 0 || o3 >= 0;
     }
+    CP_T(ct2);
     if (__ballot(in_step) == 0) {
 #pragma unroll
       for (int g = 0; g < CP_G; ++g)
@@ -462,6 +476,12 @@ __global__ __launch_bounds__(64) void copy_kernel(ResolveParams P) {
       }
     }
     wave_sync();
+    CP_T(ct3);
+    if (op + CP_STEP < n) {
+      cp_desc_fetch(dsrc, sh.desc, op + CP_STEP, n, issued, lane);
+      read_desc(op + CP_STEP);
+    }
+    CP_T(ct1);
     const uint64_t end = op + CP_STEP < n ? op + CP_STEP : n;
     if (end - flushed >= RS_FLUSH) {
       const uint64_t upto = flushed + RS_FLUSH;
@@ -474,7 +494,22 @@ __global__ __launch_bounds__(64) void copy_kernel(ResolveParams P) {
       // counted descriptor waits above only wait longer with the stores in
       // flight, never shorter)
     }
+#ifdef ZT_CP_TIME
+    CP_T(ct4);
+    cp_acc[0] += ct1 - ct3;
+    cp_acc[1] += ct2 - ct0;
+    cp_acc[2] += ct3 - ct2;
+    cp_acc[3] += ct4 - ct1;
+    ++nsteps;
+#endif
   }
+#ifdef ZT_CP_TIME
+  if (lane == 0) {
+    for (int k = 0; k < 4; ++k) atomicAdd(&g_cp_time[k], cp_acc[k]);
+    atomicAdd(&g_cp_time[6], nsteps);
+    atomicAdd(&g_cp_time[7], 1ull);
+  }
+#endif
   wave_sync();
   cp_flush(&sh, out, flushed, n, lane);
   if (lane == 0) P.seg_status[sg] = ZT_OK;
@@ -516,6 +551,15 @@ int tokenize_units_dev(const TokParams &p, hipStream_t s) {
   }
   return ZT_OK;
 }
+
+#ifdef ZT_CP_TIME
+extern "C" int zt_debug_cp_time(unsigned long long *out) {
+  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_cp_time), sizeof(unsigned long long) * 8);
+  unsigned long long z[8] = {};
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_cp_time), z, sizeof z);
+  return 0;
+}
+#endif
 
 int tok_runs_setup(DeviceCtx *c, TokParams &p, uint64_t n, hipStream_t s) {
   const uint64_t cap = n / kStoredRunMin + 64;
