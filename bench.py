@@ -101,12 +101,18 @@ def launch(nproc):
 
 
 # ---------------------------------------------------------------- helpers
+# the translation unit of the kernel the roofline reports (match_kernel) and
+# the headers it includes: a PMC measurement stays tied to that kernel's code
+DIGEST_SOURCES = ["deflate.hip", "zt_internal.h", "../../include/zt.h"]
+
+
 def source_digest():
-    """sha256 of the libzt sources (zlib.ts_amd/csrc, include/zt.h): ties a
-    PMC traffic measurement to the kernels it was taken on."""
+    """sha256 of the match kernel's sources (DIGEST_SOURCES under
+    zlib.ts_amd/csrc): ties a PMC traffic measurement to the kernel it was
+    taken on (edits to the inflate or checksum kernels leave it valid)."""
     h = hashlib.sha256()
     d = os.path.join(HERE, "zlib.ts_amd", "csrc")
-    for f in sorted(os.listdir(d)) + ["../../include/zt.h"]:
+    for f in DIGEST_SOURCES:
         with open(os.path.join(d, f), "rb") as fh:
             h.update(f.encode() + b"\0" + fh.read())
     return h.hexdigest()
