@@ -13,9 +13,9 @@ for k in wordsalad xorshift32 structured; do
   cp gpurun_out/${TAG}_$k/run_kernel_stats.csv gpurun_out/${TAG}_${k}_kernel_stats.csv
   echo "== $k: $(grep ratio gpurun_out/${TAG}_$k.log)"
   python3 -c "
-import csv
+import csv, re
 for r in csv.DictReader(open('gpurun_out/${TAG}_${k}_kernel_stats.csv')):
-    n = r['Name'].split('(')[0].replace('zt::(anonymous namespace)::', '')[:28]
+    n = re.split(r'[(<]', r['Name'].replace('zt::(anonymous namespace)::', ''))[0][:28]
     print(f'  {n:28s} {int(r[\"Calls\"]):4d} {float(r[\"AverageNs\"])/1e6:8.3f} ms')
 "
 done
