@@ -98,7 +98,8 @@ static int batch_two_phase(DeviceCtx *c, const uint8_t *d_in, const std::vector<
   tp.res = d_tres;
   tp.tokens = static_cast<uint32_t *>(d_tok);
   tp.count = (uint32_t)units;
-  tp.simt = 1;
+  static const char *simt_env = getenv("ZT_TOK_SIMT");  // (A/B: 0 = one-lane body decode)
+  tp.simt = simt_env ? atoi(simt_env) != 0 : 1;
   tp.dbg = nullptr;
   tp.dump_unit = 0xFFFFFFFFu;
   tp.dump_once = 0;
