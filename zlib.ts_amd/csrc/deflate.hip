@@ -1833,7 +1833,22 @@ __global__ __launch_bounds__(ENC_THREADS) void encode_kernel(DeflateParams P) {
       e[4] = 0xFF;
       P.slot_len[blk] = blen + 5 * nparts + 5;
     }
-    for (uint32_t i = t; i < blen; i += ENC_THREADS) slot_bytes[5 * (i / 65535 + 1) + i] = raw[i];
+    if (nparts == 1 && (reinterpret_cast<uintptr_t>(raw) & 3) == 0) {
+      // one piece: the data starts at slot byte 5, so slot word w (w >= 2)
+      // is raw bytes 4 w - 5 .. 4 w - 2 = one byte align of raw words w - 2,
+      // w - 1; words with header or marker bytes are written by the byte
+      // stores above and below
+      const uint32_t *raw32 = reinterpret_cast<const uint32_t *>(raw);
+      uint32_t *slot32 = reinterpret_cast<uint32_t *>(slot_bytes);
+      const uint32_t w_end = (blen + 5) / 4;  // words below hold data (and header) bytes only
+      for (uint32_t w = 2 + t; w < w_end; w += ENC_THREADS)
+        slot32[w] = __builtin_amdgcn_alignbyte(raw32[w - 1], raw32[w - 2], 3);
+      __syncthreads();  // (the word-wise stores land before the bytes around them)
+      if (t < 3 && t < blen) slot_bytes[5 + t] = raw[t];
+      for (uint32_t i = 4 * w_end - 5 + t; i < blen; i += ENC_THREADS) slot_bytes[5 + i] = raw[i];
+    } else {
+      for (uint32_t i = t; i < blen; i += ENC_THREADS) slot_bytes[5 * (i / 65535 + 1) + i] = raw[i];
+    }
     return;
   }
   for (uint32_t i = t; i < 288; i += ENC_THREADS) s->lit_code[i] = plan->lit_code[i];

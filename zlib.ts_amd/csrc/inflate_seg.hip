@@ -81,6 +81,17 @@ __global__ __launch_bounds__(256) void find_syncs(const uint8_t *__restrict__ in
                                                   uint64_t *__restrict__ list, uint32_t *__restrict__ count) {
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
   const int lane = threadIdx.x & 63;
+  // every span's 16-byte load in flight before the first is scanned
+  u32x4 pre[FS_ITER];
+#pragma unroll
+  for (uint32_t it = 0; it < FS_ITER; ++it) {
+    const uint64_t base =
+        (lo & ~uint64_t(15)) + (((uint64_t)blockIdx.x * FS_ITER + it) * 256 + threadIdx.x) * 16;
+    pre[it] = base + 16 <= n && (reinterpret_cast<uintptr_t>(in) & 15) == 0
+                  ? __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(in + base))
+                  : u32x4{0u, 0u, 0u, 0u};
+  }
+#pragma unroll
   for (uint32_t it = 0; it < FS_ITER; ++it) {
   const uint64_t base =
       (lo & ~uint64_t(15)) + (((uint64_t)blockIdx.x * FS_ITER + it) * 256 + threadIdx.x) * 16;
@@ -88,7 +99,7 @@ __global__ __launch_bounds__(256) void find_syncs(const uint8_t *__restrict__ in
   uint32_t w[9];
   const bool whole = base + 16 <= n && (reinterpret_cast<uintptr_t>(in) & 15) == 0;
   if (whole) {
-    const u32x4 v = *reinterpret_cast<const u32x4 *>(in + base);
+    const u32x4 v = pre[it];
     w[2] = v.x;
     w[3] = v.y;
     w[4] = v.z;
