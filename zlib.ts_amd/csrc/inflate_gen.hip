@@ -275,7 +275,7 @@ struct GenParams {
   uint32_t count;
 };
 
-__global__ __launch_bounds__(64) void gen_tokenize_kernel(GenParams P) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void gen_tokenize_kernel(GenParams P) {
   __shared__ GenShared sh;
   __shared__ SpecShared spsh;
   const uint32_t u = P.which ? P.which[blockIdx.x] : blockIdx.x;

@@ -245,6 +245,55 @@ __device__ __forceinline__ int lane_token(LaneBits &lb, const HuffTab *lt, const
   return 0;
 }
 
+// the token that starts at bit abs_bit of the round's staged input, decoded on
+// its own (its start is known: no reader state): all three words it can span
+// are read at once, so several such decodes overlap their LDS round trips.
+// Only called at a marked token start before the block's end code.
+__device__ __forceinline__ void token_at(const uint32_t *stage, uint32_t qbase, uint64_t abs_bit, const HuffTab *lt,
+                                         const HuffTab *dt, uint32_t &tok, uint32_t &nbytes) {
+  constexpr uint32_t M = (1u << PRI) - 1;
+  constexpr uint32_t QM = SP_STAGE_BYTES / 4 - 1;
+  const uint32_t q = (uint32_t)(abs_bit >> 5), sh = (uint32_t)abs_bit & 31;
+  const uint32_t w0 = stage[(q - qbase) & QM], w1 = stage[(q + 1 - qbase) & QM], w2 = stage[(q + 2 - qbase) & QM];
+  const uint64_t lo = ((uint64_t)w1 << 32) | w0;
+  uint64_t bb = sh ? (lo >> sh) | ((uint64_t)w2 << (64 - sh)) : lo;  // 64 valid bits
+  const uint32_t e = lt->pri[(uint32_t)bb & M];
+  uint32_t cl, sym, ex, base;
+  if (e & 15) {
+    cl = e & 15;
+    sym = (e >> 8) & 511;
+    ex = (e >> 4) & 15;
+    base = e >> 17;
+  } else {
+    const int s = long_code_lane(lt, (uint32_t)bb, cl);
+    sym = s < 0 ? 0u : (uint32_t)s;
+    ex = sym > 256 ? len_extra(sym - 257) : 0;
+    base = sym > 256 ? len_base(sym - 257) : 0;
+  }
+  if (sym < 256) {
+    tok = sym;
+    nbytes = 1;
+    return;
+  }
+  const uint32_t length = base + ((uint32_t)(bb >> cl) & ((1u << ex) - 1));
+  bb >>= cl + ex;
+  const uint32_t d = dt->pri[(uint32_t)bb & M];
+  uint32_t dcl, dsym, dex, dbase;
+  if (d & 15) {
+    dcl = d & 15;
+    dsym = (d >> 8) & 511;
+    dex = (d >> 4) & 15;
+    dbase = d >> 17;
+  } else {
+    const int s = long_code_lane(dt, (uint32_t)bb, dcl);
+    dsym = s < 0 ? 0u : (uint32_t)s;
+    dex = dsym < 30 ? dist_extra(dsym) : 0;
+    dbase = dsym < 30 ? dist_base(dsym) : 0;
+  }
+  tok = (length << 16) | (dbase + ((uint32_t)(bb >> dcl) & ((1u << dex) - 1)));
+  nbytes = length;
+}
+
 // lane l-1's value (lane 0: `first`), with every lane taking part (DPP wave_shr:1)
 __device__ __forceinline__ uint32_t from_prev_lane(uint32_t v, uint32_t first) {
   return (uint32_t)__builtin_amdgcn_update_dpp((int)first, (int)v, 0x138, 0xF, 0xF, false);
@@ -325,6 +374,14 @@ __device__ __forceinline__ uint64_t compose_maps(uint64_t a, uint64_t b) {
 // PHASE: phase maps for near-fixed-length codes (the sync-point / batch
 // tokenizer; the general tokenizer keeps them off: their registers cost it a
 // wave per SIMD, 3 -> 2, and its units start mid-block anyway)
+#ifdef ZT_TK_TIME
+// debug: SIMT body decode cycles (lane 0 of each wave): [0] staging, [1] pass 1,
+// [2] repairs, [3] pass 2, [4] rounds, [5] repair iterations
+__device__ unsigned long long g_tk_time[8];
+#define TK_T(v) v = __builtin_readcyclecounter()
+#else
+#define TK_T(v) (void)0
+#endif
 template <bool PHASE = false>
 __device__ int tok_huffman_simt(Reader &rd, uint64_t b0, const HuffTab *lt, const HuffTab *dt, TokOut &to,
                                 uint64_t &op, SpecShared *sp, uint64_t &end_bit, uint32_t *dump = nullptr,
@@ -345,6 +402,9 @@ __device__ int tok_huffman_simt(Reader &rd, uint64_t b0, const HuffTab *lt, cons
   const bool fixedish = PHASE && near_fixed_code(lt);
 #endif
   for (;;) {
+    [[maybe_unused]] unsigned long long tt0 = 0, tt1 = 0, tt2 = 0, tt3 = 0, tt4 = 0;
+    [[maybe_unused]] int n_iter = 0;
+    TK_T(tt0);
     // ---- stage the round's input: bytes [a0, a0 + SP_STAGE_BYTES)
     const uint64_t a0 = ((b0 + R) >> 3) & ~uint64_t(15);
     {
@@ -366,6 +426,7 @@ __device__ int tok_huffman_simt(Reader &rd, uint64_t b0, const HuffTab *lt, cons
     }
     for (uint32_t w = 0; w < SP_WORDS; ++w) sp->bm[w][lane] = 0;
     wave_sync();
+    TK_T(tt1);
     // ---- pass 1: lane l from s_l past s_{l+1}, marking token starts
     const uint32_t s_l = R + (uint32_t)lane * SP_LANE_BITS;
     const uint32_t s_next = s_l + SP_LANE_BITS;
@@ -436,6 +497,10 @@ __device__ int tok_huffman_simt(Reader &rd, uint64_t b0, const HuffTab *lt, cons
         }
       }
       wave_sync();
+#ifdef ZT_TK_TIME
+      if (iter == 0) TK_T(tt2);
+      n_iter = iter;
+#endif
       // ---- which lanes are on the true path?
       const uint32_t t = from_prev_lane(end, R);
       const uint32_t tp = t - s_l;
@@ -485,6 +550,7 @@ __device__ int tok_huffman_simt(Reader &rd, uint64_t b0, const HuffTab *lt, cons
       repair = true;
       (void)merge;
     }
+    TK_T(tt3);
     // final per-lane state: true start t, tokens = marks in [t, ev or end)
     const uint32_t t = from_prev_lane(end, R);
     const uint64_t E = __ballot(flags != 0 && ev_pos >= t && in_range);
@@ -548,8 +614,59 @@ __device__ int tok_huffman_simt(Reader &rd, uint64_t b0, const HuffTab *lt, cons
     const uint32_t idx_end = idx + my_tok;
     uint32_t my_by = 0;
     bool active = use && my_tok > 0;
-    if (active) lb.init(b0 + t, t);
     uint32_t *tokp = to.tok;
+#ifndef ZT_TK_SEQ_PASS2
+    // every token start of the lane's exact range [t, hi_p) is marked, so the
+    // tokens are decoded independently of each other (no bit position carried
+    // from one to the next), up to 4 at a time: one aligned group of 4 token
+    // indices per step, stored as one 16-byte store when the lane fills it
+    const bool vec_ok = (reinterpret_cast<uintptr_t>(tokp) & 15) == 0;
+    uint32_t mw = 0, mm = 0;  // mark word index and its unvisited marks
+    if (active) {
+      const uint32_t lo = t - s_l;
+      mw = lo >> 5;
+      mm = sp->bm[mw][lane] & (0xFFFFFFFFu << (lo & 31));
+    }
+    while (__ballot(active)) {
+      if (active) {
+        const uint32_t nk0 = 4 - (idx & 3), left = idx_end - idx;
+        const uint32_t nk = nk0 < left ? nk0 : left;
+        uint32_t xs[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          xs[k] = 0;
+          if ((uint32_t)k < nk) {
+            while (mm == 0 && mw + 1 < SP_WORDS) mm = sp->bm[++mw][lane];  // (bounded: a count mismatch cannot spin)
+            xs[k] = s_l + mw * 32 + (uint32_t)__builtin_ctz(mm);
+            mm &= mm - 1;
+          }
+        }
+        uint32_t tk[4], nb[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          tk[k] = 0;
+          nb[k] = 0;
+          if ((uint32_t)k < nk) token_at(stage, lb.qbase, b0 + xs[k], lt, dt, tk[k], nb[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          my_by += nb[k];
+          if ((uint32_t)k < nk && idx + k >= tail_base) sp->tail[(idx + k) & 63] = tk[k];
+        }
+        if (vec_ok && nk == 4) {
+          typedef unsigned int u32x4s __attribute__((ext_vector_type(4)));
+          *reinterpret_cast<u32x4s *>(tokp + idx) = u32x4s{tk[0], tk[1], tk[2], tk[3]};
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if ((uint32_t)k < nk) tokp[idx + k] = tk[k];
+        }
+        idx += nk;
+        if (idx >= idx_end) active = false;
+      }
+    }
+#else
+    if (active) lb.init(b0 + t, t);
     while (__ballot(active)) {
       if (active) {
         uint32_t tk = 0, nb = 0;
@@ -560,6 +677,7 @@ __device__ int tok_huffman_simt(Reader &rd, uint64_t b0, const HuffTab *lt, cons
         if (++idx >= idx_end) active = false;
       }
     }
+#endif
     wave_sync();
     uint32_t by = my_by;
 #pragma unroll
@@ -567,6 +685,17 @@ __device__ int tok_huffman_simt(Reader &rd, uint64_t b0, const HuffTab *lt, cons
     to.ntok = nt1;
     to.stg = sp->tail[lane];
     op += uni(by);
+#ifdef ZT_TK_TIME
+    TK_T(tt4);
+    if (lane == 0) {
+      atomicAdd(&g_tk_time[0], tt1 - tt0);
+      atomicAdd(&g_tk_time[1], tt2 - tt1);
+      atomicAdd(&g_tk_time[2], tt3 - tt2);
+      atomicAdd(&g_tk_time[3], tt4 - tt3);
+      atomicAdd(&g_tk_time[4], 1ull);
+      atomicAdd(&g_tk_time[5], (unsigned long long)n_iter);
+    }
+#endif
     if (eob) {
       end_bit = b0 + r_end;
       if (stopped) *stopped = __builtin_amdgcn_readlane(flags, e) == 3;
@@ -580,8 +709,15 @@ __device__ int tok_huffman_simt(Reader &rd, uint64_t b0, const HuffTab *lt, cons
 __device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t src_lane) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src_lane << 2), (int)v);
 }
-constexpr uint32_t RS_TOK_RING = 1024;        // tokens staged in LDS (16 chunks of 64)
-constexpr uint32_t RS_AHEAD = 12;             // chunks in flight ahead of the cursor
+#ifndef ZT_RS_TOK_RING
+#define ZT_RS_TOK_RING 1024
+#endif
+#ifndef ZT_RS_AHEAD
+#define ZT_RS_AHEAD 12
+#endif
+constexpr uint32_t RS_TOK_RING = ZT_RS_TOK_RING;  // expand: tokens staged in LDS (chunks of 64)
+constexpr uint32_t RS_AHEAD = ZT_RS_AHEAD;        // chunks in flight ahead of the cursor
+static_assert((RS_AHEAD + 2) * 64 <= RS_TOK_RING, "expand token ring");
 constexpr uint32_t RS_FLUSH = 8192;           // output flush granule
 #ifndef ZT_CP_STEP
 #define ZT_CP_STEP 512

@@ -552,6 +552,15 @@ int tokenize_units_dev(const TokParams &p, hipStream_t s) {
   return ZT_OK;
 }
 
+#ifdef ZT_TK_TIME
+extern "C" int zt_debug_tk_time(unsigned long long *out) {
+  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tk_time), sizeof(unsigned long long) * 8);
+  unsigned long long z[8] = {};
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_tk_time), z, sizeof z);
+  return 0;
+}
+#endif
+
 #ifdef ZT_CP_TIME
 extern "C" int zt_debug_cp_time(unsigned long long *out) {
   (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_cp_time), sizeof(unsigned long long) * 8);
