@@ -1,5 +1,6 @@
-# Cycle split of the match kernel per sub-chunk (libzt built with -DZT_DF_TIME, ZT_LIB=...):
-# chain build (of which serial linking), search, wait at the barrier after search.
+# Cycle split of the match kernel per wave and sub-chunk (libzt built with
+# -DZT_DF_TIME, ZT_LIB=...): hash phase, serial link (linker waves), waiting
+# for links, searching, idle at the sub-chunk barrier.
 import ctypes, os, sys; sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', 'zlib.ts_amd', 'py'))
 import torch, ztamd as zt
 buf = (ctypes.c_ulonglong * 8)()
@@ -14,6 +15,8 @@ for kind in sys.argv[1:]:
     dp.run(d_in.data_ptr(), n, d_c.data_ptr()); torch.cuda.synchronize()
     zt.lib.zt_debug_df_time(buf)
     v = list(buf)
-    subs = v[3] & ((1 << 20) - 1)
-    link = v[4]
-    print(f"{kind:10s} sub-chunks {subs}  cycles/sub: chain_build {v[0]/subs:8.0f} (link {link/subs:8.0f})  search(t0) {v[1]/subs:8.0f}  barrier wait {v[2]/subs:8.0f}", flush=True)
+    ws = v[3]  # (wave, sub-chunk) pairs
+    subs = ws / 16
+    print(f"{kind:10s} per wave per sub-chunk: hash {v[0]/ws:7.0f}  link(2 waves) {v[4]/subs/2:7.0f}  "
+          f"link-wait {v[5]/ws:7.0f}  search {v[1]/ws:7.0f}  loop total {v[7]/ws:7.0f}  barrier idle {v[2]/ws:7.0f}  "
+          f"super-steps/wave {v[6]/ws:5.2f}", flush=True)

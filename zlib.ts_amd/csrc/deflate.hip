@@ -660,7 +660,8 @@ __global__ __launch_bounds__(DF_THREADS) void match_kernel(DeflateParams P) {
 #ifdef ZT_DF_TIME
     uint64_t tl;
     DF_T(tl);
-    if (t == 0) atomicAdd(&g_df_time[4], (unsigned long long)(tl - t1));
+    if ((t & 63) == 0 && t < 128 && link) atomicAdd(&g_df_time[4], (unsigned long long)(tl - t1));
+    uint64_t t_wait = 0, t_srch = 0, n_ss = 0;
 #endif
     inserted = link ? ih : inserted;
     if (p0 >= rs) {
@@ -672,21 +673,39 @@ __global__ __launch_bounds__(DF_THREADS) void match_kernel(DeflateParams P) {
         ss = (uint32_t)__shfl((int)ss, 0, 64);
         if (ss >= nss) break;
         const uint32_t need = (p0 + 256 * (ss + 1)) < ih ? (p0 + 256 * (ss + 1)) : ih;
+#ifdef ZT_DF_TIME
+        uint64_t w0, w1, w2;
+        DF_T(w0);
+#endif
         while (min(__hip_atomic_load(&s.linked, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP),
                    __hip_atomic_load(&s.linked4, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) < need)
           __builtin_amdgcn_s_sleep(1);
+#ifdef ZT_DF_TIME
+        DF_T(w1);
+#endif
         search_quad(&s, P, p0 + 256 * ss + 4 * (t & 63), p0, p1, key, res_out);
+#ifdef ZT_DF_TIME
+        DF_T(w2);
+        t_wait += w1 - w0;
+        t_srch += w2 - w1;
+        n_ss += 1;
+#endif
       }
     }
     DF_T(t2);
     lds_barrier();
     DF_T(t3);
 #ifdef ZT_DF_TIME
-    if (t == 0) {
+    // per wave (lane 0): hash phase, searching, barrier wait, (wave, sub-chunk)
+    // pairs, link waits, super-steps, link + search loop
+    if ((t & 63) == 0) {
       atomicAdd(&g_df_time[0], (unsigned long long)(t1 - t0));
-      atomicAdd(&g_df_time[1], (unsigned long long)(t2 - t1));
+      atomicAdd(&g_df_time[1], (unsigned long long)t_srch);
       atomicAdd(&g_df_time[2], (unsigned long long)(t3 - t2));
       atomicAdd(&g_df_time[3], 1ull);
+      atomicAdd(&g_df_time[5], (unsigned long long)t_wait);
+      atomicAdd(&g_df_time[6], (unsigned long long)n_ss);
+      atomicAdd(&g_df_time[7], (unsigned long long)(t2 - t1));
     }
 #endif
     if (fast) {
