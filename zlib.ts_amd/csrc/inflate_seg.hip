@@ -338,8 +338,13 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
     if (r.status != ZT_OK || r.out_len > 0xFFFFFFFFull)
       FALLBACK("unit %zu (chain %zu): status %d detail %d ntok %u out %llu\n", u, chain.size(), r.status,
                r.detail, r.ntok, (unsigned long long)r.out_len);
+    // (a restart point right after another -- the empty stored blocks of a
+    // restart marker -- leaves the segment before it empty: that one simply
+    // starts here instead.  Empty copy waves would sit between the full ones
+    // in the launch, and the workgroup -> XCD round robin would then give
+    // half of the XCDs every 1 MiB segment: two rounds of copy waves.)
     const bool seg_start_here = u == 0 || restart[u - 1];
-    if (seg_start_here || segs.empty()) {
+    if (segs.empty() || (seg_start_here && total != seg_start)) {
       desc_total = (desc_total + 511) & ~uint64_t(511);
       desc_seg = desc_total;
       seg_start = total;
@@ -357,6 +362,20 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   }
   *out_len = total;
   *end_ip = (res[u].end_bits + 7) >> 3;
+  if (inf_debug()) {
+    // segment sizes (copy_kernel: one wave per segment)
+    uint64_t mn = ~0ull, mx = 0;
+    size_t small = 0;
+    for (size_t i = 0; i < segs.size(); ++i) {
+      const ChainUnit &a = chain[segs[i].first], &b = chain[segs[i].first + segs[i].count - 1];
+      const uint64_t len = b.out_off + b.out_len - a.out_off;
+      mn = len < mn ? len : mn;
+      mx = len > mx ? len : mx;
+      small += len < (512u << 10);
+    }
+    fprintf(stderr, "[zt inflate] %zu units, %zu segments, %llu bytes: segment min %llu max %llu, %zu under 512 KiB\n",
+            chain.size(), segs.size(), (unsigned long long)total, (unsigned long long)mn, (unsigned long long)mx, small);
+  }
   uint8_t *d_out = *d_out_io;
   if (!d_out) {  // caller wants a library-owned buffer (scratch slot 1)
     void *p;
