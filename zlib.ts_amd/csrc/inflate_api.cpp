@@ -103,7 +103,7 @@ static int batch_two_phase(DeviceCtx *c, const uint8_t *d_in, const std::vector<
   tp.dbg = nullptr;
   tp.dump_unit = 0xFFFFFFFFu;
   tp.dump_once = 0;
-  ZT_TRY(tok_runs_setup(c, tp, in_hi, s));
+  tp.run_tokens = 1;
   BT("tokenize launch");
   ZT_TRY(tokenize_units_dev(tp, s));
   std::vector<TokResult> tr(units);
@@ -153,6 +153,7 @@ static int batch_two_phase(DeviceCtx *c, const uint8_t *d_in, const std::vector<
   rp.nunits = (uint32_t)chain.size();
   rp.nseg = (uint32_t)segs.size();
   rp.marker = 0;
+  rp.in = d_in;
   ZT_TRY(resolve_segments_dev(rp, s));
   std::vector<int32_t> ust(chain.size()), sst(segs.size());
   ZT_HIP(hipMemcpyAsync(ust.data(), d_ust, chain.size() * 4, hipMemcpyDeviceToHost, s));

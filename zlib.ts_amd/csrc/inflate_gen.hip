@@ -1210,6 +1210,7 @@ int inflate_general_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t inde
   rp.nunits = (uint32_t)chain.size();
   rp.nseg = (uint32_t)segs.size();
   rp.marker = 1;
+  rp.in = nullptr;  // (the general tokenizer writes no run tokens)
   ZT_TRY(expand_units_dev(rp, s));
   uint16_t *o16 = static_cast<uint16_t *>(d_o16);
   copy_marker_kernel<<<rp.nseg, 64, 0, s>>>(rp, d_gs, o16);

@@ -286,7 +286,7 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   }
   tp.dump_unit = getenv("ZT_TOK_DUMP") ? (uint32_t)atoi(getenv("ZT_TOK_DUMP")) : 0xFFFFFFFFu;
   tp.dump_once = 0;
-  ZT_TRY(tok_runs_setup(c, tp, n, s));
+  tp.run_tokens = 1;
   ZT_TRY(timing_begin(c, s, 3));
   ZT_TRY(tokenize_units_dev(tp, s));
   ZT_TRY(timing_end(c, s, 3));
@@ -416,6 +416,7 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   rp.nunits = (uint32_t)chain.size();
   rp.nseg = (uint32_t)segs.size();
   rp.marker = 0;
+  rp.in = d_in;
   ZT_TRY(resolve_segments_dev(rp, s));
   ZT_TRY(timing_end(c, s, 2));
   ZT_HIP(hipMemcpyAsync(h_ust, d_ust, chain.size() * 4, hipMemcpyDeviceToHost, s));

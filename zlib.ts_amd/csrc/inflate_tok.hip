@@ -64,6 +64,7 @@ __global__ __launch_bounds__(64) ZT_TOK_ATTR void tokenize_kernel(TokParams P) {
   int status = ZT_OK, detail = 0, stop_idx = -1;
   uint64_t si = job.stop_first;
   bool bfinal = false;
+  bool any_run = false;  // run tokens written (flag bit 31 of the result's ntok: expand_kernel's run path)
   g_u8 *gin = (g_u8 *)P.in;
   while (!bfinal) {
     uint32_t v;
@@ -92,29 +93,21 @@ __global__ __launch_bounds__(64) ZT_TOK_ATTR void tokenize_kernel(TokParams P) {
         break;
       }
       if (len) {
-        to.flush_partial();
-        // a long payload is handed to stored_fill_kernel (wide copies after
-        // this kernel); every lane takes part in the claim (no lane-0 branch
-        // inside the block loop), lane 0 adding the one
-        bool inline_copy = true;
-        if (P.runs && len >= kStoredRunMin) {
-          const uint32_t k = uni(atomicAdd(P.nruns, lane == 0 ? 1u : 0u));
-          if (k < P.runs_cap) {
-            inline_copy = false;
-            StoredRun r;  // (every lane stores the same record)
-            r.src = p;
-            r.dst = (uint64_t)(to.tok - P.tokens) + nt0;
-            r.len = len;
-            r.pad = 0;
-            P.runs[k] = r;
-          }
-        }
-        if (inline_copy)
+        if (P.run_tokens && len >= kStoredRunMin) {
+          // a long payload stays in the input: three run tokens, and
+          // expand_kernel writes its literal descriptors from there
+          to.emit(len << 16);
+          to.emit((uint32_t)p);
+          to.emit((uint32_t)(p >> 32));
+          any_run = true;
+        } else {
+          to.flush_partial();
           for (uint32_t j = lane; j < len; j += 64) to.tok[nt0 + j] = gin[p + j];
-        const uint32_t nt = nt0 + len;
-        const uint32_t idx = (nt & ~63u) + (uint32_t)lane;
-        if ((uint32_t)lane < (nt & 63) && idx >= nt0) to.stg = gin[p + idx - nt0];
-        to.ntok = nt;
+          const uint32_t nt = nt0 + len;
+          const uint32_t idx = (nt & ~63u) + (uint32_t)lane;
+          if ((uint32_t)lane < (nt & 63) && idx >= nt0) to.stg = gin[p + idx - nt0];
+          to.ntok = nt;
+        }
         op += len;
       }
       rd.seek_byte(p + len);
@@ -181,7 +174,7 @@ __global__ __launch_bounds__(64) ZT_TOK_ATTR void tokenize_kernel(TokParams P) {
     TokResult r;
     r.out_len = op;
     r.end_bits = rd.pos_bits_in();
-    r.ntok = to.ntok;
+    r.ntok = to.ntok | (any_run ? 0x80000000u : 0u);
     r.status = status;
     r.detail = detail;
     r.stop_idx = stop_idx;
@@ -235,13 +228,14 @@ struct ExpandShared {
   uint16_t cw[CP_STEP];        // descriptors of the current copy step
 };
 
-__global__ __launch_bounds__(64) void expand_kernel(ResolveParams P) {
-  __shared__ ExpandShared sh;
+// RUNS: the unit holds run tokens (ChainUnit ntok bit 31); units without
+// them take the loop without the run checks
+template <bool RUNS>
+__device__ __forceinline__ void expand_unit(const ResolveParams &P, ExpandShared &sh, const ChainUnit &cu) {
   const uint32_t u = blockIdx.x;
   const int lane = threadIdx.x & 63;
-  const ChainUnit cu = P.units[u];
   const uint32_t *tk = P.tokens + cu.tok_off;
-  const uint32_t ntok = cu.ntok;
+  const uint32_t ntok = cu.ntok & 0x7FFFFFFFu;
   const uint32_t nchunks = (ntok + 63) / 64;
   uint16_t *desc = P.desc + cu.desc_off;
   const uint64_t back = cu.out_off - cu.seg_off;  // bytes of the segment before this unit
@@ -267,13 +261,54 @@ __global__ __launch_bounds__(64) void expand_kernel(ResolveParams P) {
     const uint32_t ti = cur + (uint32_t)lane;
     const bool valid = ti < ntok;
     const uint32_t t = sh.tok[ti & (RS_TOK_RING - 1)];
+    // a stored run at the cursor (tokenize_kernel: len << 16 with distance 0,
+    // then the payload's input offset in two tokens): its literal descriptors
+    // straight from the input, 8 bytes per lane in flight
+    const uint32_t t0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
+    if (RUNS && rem == 0 && (t0 >> 16) != 0 && (t0 & 0xFFFFu) == 0) {
+      const uint32_t rl = t0 >> 16;
+      const uint64_t src = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)t, 1) |
+                           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)t, 2) << 32);
+      const uint8_t *sp = P.in + src;
+      for (uint32_t i0 = 0; i0 < rl; i0 += 512) {
+        uint32_t b[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uint32_t i = i0 + 64 * k + (uint32_t)lane;
+          b[k] = i < rl ? sp[i] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uint32_t i = i0 + 64 * k + (uint32_t)lane;
+          if (i < rl) desc[op + i] = (uint16_t)(0x8000u | b[k]);
+        }
+      }
+      // the copy step holding the run's end keeps its descriptors for the
+      // references of the tokens after it
+      const uint64_t pos = back + op, e = pos + rl;
+      const uint64_t ws_e = (e - 1) & ~uint64_t(CP_STEP - 1);
+      for (uint64_t x = (pos > ws_e ? pos : ws_e) + (uint64_t)lane; x < e; x += 64)
+        sh.cw[x - ws_e] = (uint16_t)(0x8000u | sp[x - pos]);
+      wave_sync();
+      op += rl;
+      cur += 3;
+      continue;
+    }
     const uint32_t len = valid ? tok_len(t) : 0u;
     const uint32_t S = wave_incl_scan(len);
     const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)S, 63) - rem;
     // windows coincide with copy_kernel's 64-byte steps of the segment
     const uint64_t pos = back + op;  // segment position of this window's first byte
     const uint32_t room = 64 - (uint32_t)(pos & 63);
-    const uint32_t W = total < room ? total : room;
+    uint32_t W = total < room ? total : room;
+    // a window ends where a stored run starts (the run is taken at the
+    // cursor); the run's two offset tokens after it are never scanned into one
+    const uint64_t runs = RUNS ? __ballot(valid && (t >> 16) != 0 && (t & 0xFFFFu) == 0) : 0ull;
+    if (RUNS && runs) {
+      const int fl = __ffsll((long long)runs) - 1;  // >= 1: a run at the cursor was taken above
+      const uint32_t rs = (uint32_t)__builtin_amdgcn_readlane((int)(S - len), fl) - rem;
+      W = rs < W ? rs : W;
+    }
     const uint64_t ws = pos & ~uint64_t(CP_STEP - 1);
     ++seq;
     const int32_t p = (int32_t)S - (int32_t)rem;
@@ -345,6 +380,15 @@ __global__ __launch_bounds__(64) void expand_kernel(ResolveParams P) {
   }
   const bool any_bad = __ballot(bad) != 0;
   if (lane == 0) P.unit_status[u] = any_bad ? ZT_E_INVALID_DISTANCE : (op != cu.out_len ? ZT_E_INPUT_BROKEN : ZT_OK);
+}
+
+__global__ __launch_bounds__(64) void expand_kernel(ResolveParams P) {
+  __shared__ ExpandShared sh;
+  const ChainUnit cu = P.units[blockIdx.x];
+  if (cu.ntok >> 31)
+    expand_unit<true>(P, sh, cu);
+  else
+    expand_unit<false>(P, sh, cu);
 }
 
 
@@ -515,40 +559,12 @@ __global__ __launch_bounds__(64) void copy_kernel(ResolveParams P) {
   if (lane == 0) P.seg_status[sg] = ZT_OK;
 }
 
-// stored payloads -> literal tokens: one run per workgroup (grid-stride),
-// 8 byte loads per thread in flight (HBM: 1 byte read + 4 written per byte)
-constexpr int kFillGrid = 2048;
-__global__ __launch_bounds__(256) void stored_fill_kernel(const uint8_t *__restrict__ in,
-                                                          const StoredRun *__restrict__ runs,
-                                                          const uint32_t *__restrict__ nruns, uint32_t cap,
-                                                          uint32_t *__restrict__ tok) {
-  const uint32_t cnt = *nruns < cap ? *nruns : cap;
-  for (uint32_t r = blockIdx.x; r < cnt; r += gridDim.x) {
-    const StoredRun R = runs[r];
-    const uint8_t *src = in + R.src;
-    uint32_t *dst = tok + R.dst;
-    uint32_t i = threadIdx.x;
-    for (; i + 7 * 256 < R.len; i += 8 * 256) {
-      uint32_t b[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) b[k] = src[i + 256 * k];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) dst[i + 256 * k] = b[k];
-    }
-    for (; i < R.len; i += 256) dst[i] = src[i];
-  }
-}
-
 }  // namespace
 
 int tokenize_units_dev(const TokParams &p, hipStream_t s) {
   if (p.count == 0) return ZT_OK;
   tokenize_kernel<<<p.count, 64, 0, s>>>(p);
   ZT_HIP(hipGetLastError());
-  if (p.runs) {
-    stored_fill_kernel<<<kFillGrid, 256, 0, s>>>(p.in, p.runs, p.nruns, p.runs_cap, p.tokens);
-    ZT_HIP(hipGetLastError());
-  }
   return ZT_OK;
 }
 
@@ -569,17 +585,6 @@ extern "C" int zt_debug_cp_time(unsigned long long *out) {
   return 0;
 }
 #endif
-
-int tok_runs_setup(DeviceCtx *c, TokParams &p, uint64_t n, hipStream_t s) {
-  const uint64_t cap = n / kStoredRunMin + 64;
-  void *buf;
-  ZT_TRY(scratch(c, 21, 256 + cap * sizeof(StoredRun), &buf));
-  p.nruns = static_cast<uint32_t *>(buf);
-  p.runs = reinterpret_cast<StoredRun *>(static_cast<uint8_t *>(buf) + 256);
-  p.runs_cap = (uint32_t)(cap < 0xFFFFFFFFull ? cap : 0xFFFFFFFFull);
-  ZT_HIP(hipMemsetAsync(p.nruns, 0, 4, s));
-  return ZT_OK;
-}
 
 int expand_units_dev(const ResolveParams &p, hipStream_t s) {
   if (p.nunits == 0) return ZT_OK;

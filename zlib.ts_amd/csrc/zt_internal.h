@@ -218,14 +218,6 @@ struct TokResult {
   int32_t detail;
   int32_t stop_idx;   // sync point where the unit stopped, -1 at BFINAL
 };
-// a stored block's payload, copied into its literal tokens by
-// stored_fill_kernel after tokenize_kernel (the tokenizer only reserves them)
-struct StoredRun {
-  uint64_t src;  // input byte offset of the payload
-  uint64_t dst;  // token index of its first byte
-  uint32_t len;
-  uint32_t pad;
-};
 struct TokParams {
   const uint8_t *in;
   uint64_t n;
@@ -239,13 +231,13 @@ struct TokParams {
   uint64_t *dbg;      // debug: per unit 8 words comparing the SIMT and scalar body decodes, or null
   uint32_t dump_unit; // debug: unit whose first SIMT block dumps per-round lane state after dbg[count * 8]
   uint32_t dump_once;
-  StoredRun *runs;    // stored payloads of >= kStoredRunMin bytes (null: the tokenizer copies every one)
-  uint32_t *nruns;    // records claimed (may pass runs_cap: those payloads are copied inline)
-  uint32_t runs_cap;
+  // stored payloads of >= kStoredRunMin bytes become three *run tokens*
+  // (len << 16 with distance 0, then the payload's input offset, low and high
+  // words) whose literal descriptors expand_kernel writes straight from the
+  // input; 0: the tokenizer writes a literal token per stored byte
+  int run_tokens;
 };
 constexpr uint32_t kStoredRunMin = 1024;
-// Scratch slot 21 for the stored runs of an n-byte input; sets p.runs / nruns / runs_cap.
-int tok_runs_setup(DeviceCtx *c, TokParams &p, uint64_t n, hipStream_t s);
 // phase B: units of the chain, grouped by segment
 struct ChainUnit {
   uint64_t tok_off;
@@ -269,6 +261,7 @@ struct ResolveParams {
   uint32_t nunits;
   uint32_t nseg;
   int32_t marker;        // expand: segments after the first may reach up to 32 KiB behind their start
+  const uint8_t *in;     // expand: the compressed input (payloads of run tokens)
 };
 int tokenize_units_dev(const TokParams &p, hipStream_t s);
 int resolve_segments_dev(const ResolveParams &p, hipStream_t s);
