@@ -64,6 +64,12 @@ static int batch_two_phase(DeviceCtx *c, const uint8_t *d_in, const std::vector<
       failed.push_back(i);
   }
   if (ids.empty()) return ZT_OK;
+  // longest input first: one wave per stream, and workgroups go to the 8 XCDs
+  // round robin -- a batch alternating slow and fast streams (C2: random-data
+  // and text blocks) would otherwise put every slow one on half of the XCDs
+  std::stable_sort(ids.begin(), ids.end(), [&](size_t a, size_t b) {
+    return n[a] - (index ? index[a] : 0) > n[b] - (index ? index[b] : 0);
+  });
   const size_t units = ids.size();
   std::vector<TokJob> jobs(units);
   uint64_t tok_total = 0, in_hi = 0;
