@@ -24,6 +24,7 @@
 // stream with one wave (inflate.hip), which also yields the reference's
 // exact error.  Results are identical to the sequential decode by
 // construction.  Replaces src/RawInflate.ts:127-143 for such streams.
+#include <chrono>
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -183,8 +184,19 @@ __global__ __launch_bounds__(256) void unit_jobs(const uint64_t *__restrict__ ke
 
 }  // namespace
 
+// ZT_INF_TIMING=1: host wall time of inflate_segments_dev's stages on stderr (measurement only)
+static double it_now() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+#define IT(label)                                                   \
+  do {                                                              \
+    static const bool on_ = getenv("ZT_INF_TIMING") != nullptr;     \
+    if (on_) fprintf(stderr, "[inflate] %-24s %9.3f ms\n", label, it_now()); \
+  } while (0)
+
 int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t index, uint8_t **d_out_io,
                          size_t out_cap, size_t *out_len, size_t *end_ip, hipStream_t s) {
+  IT("start");
   if (n < index + (1u << 14)) return 1;  // small: one wave is as fast
   // 1. sync points
   void *d_cand;
@@ -200,6 +212,7 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   uint32_t cnt = 0;
   ZT_HIP(hipMemcpyAsync(&cnt, d_count, 4, hipMemcpyDeviceToHost, s));
   ZT_HIP(hipStreamSynchronize(s));
+  IT("sync points counted");
   if (cnt == 0 || cnt > kMaxSync) FALLBACK("%u sync points\n", cnt);
   // 2. the candidates sorted, deduplicated and turned into units on the
   // device (hipcub radix sort + scan): unit 0 starts at `index`, unit k + 1
@@ -241,6 +254,7 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   uint32_t nsync = 0;
   ZT_HIP(hipMemcpyAsync(&nsync, d_pos + cnt, 4, hipMemcpyDeviceToHost, s));
   ZT_HIP(hipStreamSynchronize(s));
+  IT("units counted");
   const size_t units = (size_t)nsync + 1;
   // Every candidate sync point gets a token slot before the chain shows which
   // are real block boundaries, so a stream whose stored data is full of the
@@ -251,9 +265,13 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   // (a highly compressible stream needs far more token bytes than its own
   // size -- ~4 bytes per output byte -- so the budget is the device's free
   // memory, not a multiple of the input)
-  size_t mem_free = 0, mem_total = 0;
-  ZT_HIP(hipMemGetInfo(&mem_free, &mem_total));
-  if (tok_bytes > c->buf_size[4] + mem_free / 2) FALLBACK("%zu sync candidates: token slots over budget\n", units);
+  // (only asked when the cached slots are too small: hipMemGetInfo is a
+  // driver round trip on every call otherwise)
+  if (tok_bytes > c->buf_size[4]) {
+    size_t mem_free = 0, mem_total = 0;
+    ZT_HIP(hipMemGetInfo(&mem_free, &mem_total));
+    if (tok_bytes > c->buf_size[4] + mem_free / 2) FALLBACK("%zu sync candidates: token slots over budget\n", units);
+  }
   void *d_tok;
   if (scratch(c, 4, tok_bytes, &d_tok) != ZT_OK) FALLBACK("token slots (%zu B) not allocated\n", tok_bytes);
   // metadata comes back through pinned staging (slot 1):
@@ -294,6 +312,7 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   ZT_HIP(hipMemcpyAsync(pin, d_restart, nsync, hipMemcpyDeviceToHost, s));
   ZT_HIP(hipMemcpyAsync(res, d_res, units * sizeof(TokResult), hipMemcpyDeviceToHost, s));
   ZT_HIP(hipStreamSynchronize(s));
+  IT("tokenized");
   if (check) {
     std::vector<uint64_t> dbg(units * 8);
     ZT_HIP(hipMemcpy(dbg.data(), tp.dbg, units * 64, hipMemcpyDeviceToHost));
@@ -417,11 +436,13 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   rp.nseg = (uint32_t)segs.size();
   rp.marker = 0;
   rp.in = d_in;
+  IT("chain built");
   ZT_TRY(resolve_segments_dev(rp, s));
   ZT_TRY(timing_end(c, s, 2));
   ZT_HIP(hipMemcpyAsync(h_ust, d_ust, chain.size() * 4, hipMemcpyDeviceToHost, s));
   ZT_HIP(hipMemcpyAsync(h_st, d_st, segs.size() * 4, hipMemcpyDeviceToHost, s));
   ZT_HIP(hipStreamSynchronize(s));
+  IT("resolved");
   ZT_TRY(timing_collect(c, &c->times.inflate_ms, &c->times.inflate_launches, 2));
   ZT_TRY(timing_collect(c, &c->times.inflate_tok_ms, &c->times.inflate_toks, 3));
   for (size_t i = 0; i < chain.size(); ++i)
