@@ -77,11 +77,22 @@ __device__ __forceinline__ uint32_t fs_word(const uint8_t *in, uint64_t n, int64
   }
   return v;
 }
-constexpr uint32_t FS_ITER = 4;  // 4 KiB spans per workgroup (fewer, longer workgroups)
+#ifndef ZT_FS_ITER
+#define ZT_FS_ITER 4
+#endif
+constexpr uint32_t FS_ITER = ZT_FS_ITER;  // 4 KiB spans per workgroup (fewer, longer workgroups)
+constexpr uint32_t kFsLocal = 64;  // sync candidates a workgroup gathers before its one global atomic
+#ifndef ZT_FS_NT
+#define ZT_FS_NT 1
+#endif
 __global__ __launch_bounds__(256) void find_syncs(const uint8_t *__restrict__ in, uint64_t lo, uint64_t n,
                                                   uint64_t *__restrict__ list, uint32_t *__restrict__ count) {
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
   const int lane = threadIdx.x & 63;
+  __shared__ uint32_t s_n, s_base;
+  __shared__ uint64_t s_list[kFsLocal];
+  if (threadIdx.x == 0) s_n = 0;
+  __syncthreads();
   // every span's 16-byte load in flight before the first is scanned
   u32x4 pre[FS_ITER];
 #pragma unroll
@@ -89,7 +100,8 @@ __global__ __launch_bounds__(256) void find_syncs(const uint8_t *__restrict__ in
     const uint64_t base =
         (lo & ~uint64_t(15)) + (((uint64_t)blockIdx.x * FS_ITER + it) * 256 + threadIdx.x) * 16;
     pre[it] = base + 16 <= n && (reinterpret_cast<uintptr_t>(in) & 15) == 0
-                  ? __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(in + base))
+                  ? (ZT_FS_NT ? __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(in + base))
+                             : *reinterpret_cast<const u32x4 *>(in + base))
                   : u32x4{0u, 0u, 0u, 0u};
   }
 #pragma unroll
@@ -138,12 +150,26 @@ __global__ __launch_bounds__(256) void find_syncs(const uint8_t *__restrict__ in
       if (p > lo && p < n) {
         // bytes base + j - 6 .. base + j - 1: 00 00 00 FF FF 00
         const bool restart = base + j >= 6 && at(2 + j) == 0xFF000000u && (at(6 + j) & 0xFFFFu) == 0x00FFu;
-        const uint32_t k = atomicAdd(count, 1u);
-        if (k < kMaxSync) list[k] = (p << 1) | (restart ? 1 : 0);
+        // gathered per workgroup (one global atomic per workgroup: hits
+        // from every workgroup on one counter serialise at its L2 slice)
+        const uint64_t v = (p << 1) | (restart ? 1 : 0);
+        const uint32_t k = atomicAdd(&s_n, 1u);
+        if (k < kFsLocal) {
+          s_list[k] = v;
+        } else {
+          const uint32_t g = atomicAdd(count, 1u);
+          if (g < kMaxSync) list[g] = v;
+        }
       }
     }
   }
   }
+  __syncthreads();
+  const uint32_t m = s_n < kFsLocal ? s_n : kFsLocal;
+  if (threadIdx.x == 0 && m) s_base = atomicAdd(count, m);
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < m; i += 256)
+    if (s_base + i < kMaxSync) list[s_base + i] = s_list[i];
 }
 
 size_t align256(size_t v) { return (v + 255) & ~size_t(255); }
