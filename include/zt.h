@@ -311,9 +311,19 @@ typedef struct {
    * points), [2] one wave per stream */
   uint64_t inflate_paths[3];
   uint64_t general_passes; /* decode passes of the general path (1 = no redo) */
+  /* deflate blocks whose bytes cannot beat a stored block (order-0 entropy
+   * and no repeats): stored without a match search (counted whether timing
+   * is on or not) */
+  uint64_t blocks_unsearched;
 } zt_kernel_times;
 int zt_timing_enable(int on); /* resets the counters */
 int zt_timing_read(zt_kernel_times *out);
+/* Device scratch and pinned host staging the calling thread's device context
+ * holds (grow-only caches reused by later calls), and a call that gives them
+ * back (engine extension: the reference allocates per call, nothing is
+ * cached). */
+int zt_scratch_bytes(size_t *device_bytes, size_t *pinned_bytes);
+int zt_release_scratch(void);
 
 #ifdef __cplusplus
 }

@@ -178,7 +178,20 @@ def test_segment_false_candidates(zt, oracle):
     # a Huffman stream followed by stored data holding the pattern
     d2 = oracle.gen("wordsalad", 4, 1 << 19) + pat * 40000 + oracle.gen("xorshift32", 4, 1 << 19)
     s2 = zt.deflate_raw(d2)
+    zt.release_scratch()
     assert zt.inflate_raw(s2)[0] == d2
+    # every false candidate's token slot is bounded by the input bits up to
+    # the next candidate: ~80 K candidates must not take a block's slot each
+    # (~10 GB); the whole call stays well under 1 GiB of scratch
+    dev, _ = zt.scratch_bytes()
+    assert dev < (1 << 30), dev
+    # a crafted input that is nothing but dense candidates
+    junk = pat * 400000
+    zt.release_scratch()
+    with pytest.raises(zt.ZtError):
+        zt.inflate_raw(junk)
+    dev, _ = zt.scratch_bytes()
+    assert dev < (1 << 30), dev
     # truncated segmented stream: same error as the one-wave decode
     s3 = zt.deflate_raw(oracle.gen("wordsalad", 5, 3 << 20))
     with pytest.raises(zt.ZtError):

@@ -1,12 +1,12 @@
 """Config C4: GZip end-to-end of a 10 000-file batch, sizes
-log-uniform 1 KiB - 1 MiB, mixed text / binary, through zt_gzip_compress_batch
+log-uniform 1 KiB - 1 MiB, half text / half binary (tests/c4_corpus.py, the
+batch tests/test_gpu_c4.py checks), through zt_gzip_compress_batch
 (host buffers in, malloc'd members out: PCIe and host framing included) on
 every visible GPU (zt_set_devices) -- and on one.  Members are verified with
 zlib (an independent inflater) and a sample with the oracle's RawInflate.
    usage: python tools/c4_batch.py [files] [out.json]"""
 import ctypes
 import json
-import math
 import os
 import random
 import sys
@@ -18,16 +18,11 @@ sys.path.insert(0, os.path.join(HERE, "..", "tests"))
 sys.path.insert(0, os.path.join(HERE, "..", "zlib.ts_amd", "py"))
 import zt_oracle  # noqa: E402
 import ztamd  # noqa: E402
+from c4_corpus import c4_files  # noqa: E402
 
 
 def corpus(o, count, seed=1):
-    rng = random.Random(seed)
-    kinds = ["wordsalad", "xorshift32", "structured"]
-    files = []
-    for i in range(count):
-        n = int(math.exp(rng.uniform(math.log(1 << 10), math.log(1 << 20))))
-        files.append(o.gen(kinds[i % 3], seed * 100003 + i, n))
-    return files
+    return c4_files(o, count, seed)
 
 
 def run(files, reps=3):

@@ -128,6 +128,10 @@ struct DeflateParams {
   // whole blocks from a 32 KiB-aligned offset; per block the [start, end) of
   // its stream (relative to halo = 0), or null for one stream of n bytes
   const uint64_t *span;
+  // per block: 1 = no match search, a stored block (classify_kernel: bytes
+  // that cannot beat stored); null when not classified
+  uint8_t *store;
+  uint32_t *nstore;     // blocks flagged (one counter, zeroed before classify_kernel)
   uint32_t *res;        // n: per-position match, then (in place) per-block tokens
   uint8_t *slots;       // nblocks x DF_SLOT
   uint32_t *slot_len;   // nblocks
@@ -192,6 +196,115 @@ __device__ __forceinline__ uint32_t len_sym(uint32_t L) {  // 0..28 (symbol - 25
   uint32_t x = L - 3;
   uint32_t k = 31 - __clz(x);  // >= 3
   return 4 * (k - 1) + ((x >> (k - 2)) & 3);
+}
+
+// ================================ 0. classify_kernel ================================
+// Blocks that cannot beat a stored block skip the match search and the parse
+// (src/RawDeflate.ts:122-153 is the stored form).  Decided
+// from the block's bytes alone, one 256-thread workgroup per 32 KiB block:
+//  A. order-0 entropy of a 4 KiB sample (16 bytes every blen / 256): below
+//     CL_ENTROPY bits per byte the literals alone would compress -> search;
+//  B. high-entropy blocks are checked for repeats (random data that occurs
+//     twice compresses although its bytes look random): the 8-byte keys of
+//     every 16th position of the window (up to 28 KiB of history in the same
+//     segment + the block) go into an LDS table, every position of the block
+//     looks its key up; a repeat of L bytes gives ~L / 16 hits (the pair's
+//     other position, before or after, within a match distance).  CL_HITS hits
+//     or more -> search.
+// Everything else is flagged: match / price / DP / parse skip the block and
+// block_kernel plans it stored (the smallest form for such bytes: the
+// reference's dynamic block of random data is 0.1 % larger).
+constexpr float CL_ENTROPY = 7.85f;  // uniform bytes: ~7.955 from a 4096-byte sample
+constexpr uint32_t CL_HITS = 8;
+constexpr uint32_t CL_TABLE = 8192;
+constexpr uint32_t CL_WIN = DF_HIST + DF_BLOCK;  // history + block
+struct ClassifyShared {
+  uint32_t data[CL_WIN / 4 + 4];
+  uint16_t table[CL_TABLE];
+  uint32_t hist[256];
+  float part[4];
+  uint32_t hits[4];
+};
+
+__device__ __forceinline__ uint32_t cl_word(const uint32_t *w, uint32_t r) {
+  return __builtin_amdgcn_alignbyte(w[(r >> 2) + 1], w[r >> 2], r & 3);
+}
+
+__global__ __launch_bounds__(256) void classify_kernel(DeflateParams P) {
+  __shared__ ClassifyShared sh;
+  ClassifyShared *s = &sh;
+  const uint32_t t = threadIdx.x, blk = blockIdx.x;
+  const uint64_t lo = (uint64_t)blk * DF_BLOCK;
+  const uint64_t n = stream_end(P, blk);
+  const uint32_t blen = (uint32_t)((n - lo) < DF_BLOCK ? (n - lo) : DF_BLOCK);
+  const uint8_t *g = P.base + P.halo;  // stream byte 0
+  if (blen < 4096) {  // (small blocks: a search is cheap)
+    if (t == 0) P.store[blk] = 0;
+    return;
+  }
+  // A. entropy of the sample
+  s->hist[t] = 0;
+  __syncthreads();
+  const uint32_t stride = blen / 256;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) atomicAdd(&s->hist[g[lo + (uint64_t)t * stride + j]], 1u);
+  __syncthreads();
+  const float c = (float)s->hist[t];
+  float e = c > 0.f ? c * __log2f(c) : 0.f;
+  for (int off = 32; off; off >>= 1) e += __shfl_xor(e, off, 64);
+  if ((t & 63) == 0) s->part[t >> 6] = e;
+  __syncthreads();
+  const float h = 12.0f - (s->part[0] + s->part[1] + s->part[2] + s->part[3]) * (1.0f / 4096.0f);
+  if (h < CL_ENTROPY) {
+    if (t == 0) P.store[blk] = 0;
+    return;
+  }
+  // B. repeats inside the window: history from the block's segment / stream
+  const uint64_t f_lo = P.span ? P.span[2 * (uint64_t)blk] : 0;
+  const uint64_t seg = ((lo - f_lo) / DF_BLOCK) / P.restart;
+  uint64_t w_lo = f_lo + seg * P.restart * DF_BLOCK;  // segment start (stream coordinates)
+  const bool halo_hist = !P.span && seg == 0 && P.halo > 0;  // the first segment may look into the halo
+  int64_t h0 = (int64_t)lo - DF_HIST;
+  const int64_t floor_ = halo_hist ? -(int64_t)(P.halo < (uint64_t)DF_HIST ? P.halo : (uint64_t)DF_HIST) : (int64_t)w_lo;
+  if (h0 < floor_) h0 = floor_;
+  const uint32_t wlen = (uint32_t)((int64_t)lo + blen - h0);
+  const uint8_t *wg = g + h0;
+  uint8_t *db = reinterpret_cast<uint8_t *>(s->data);
+  if ((reinterpret_cast<uintptr_t>(wg) & 3) == 0) {
+    const uint32_t *w32 = reinterpret_cast<const uint32_t *>(wg);
+    for (uint32_t i = t; i < wlen / 4; i += 256) s->data[i] = w32[i];
+    for (uint32_t i = (wlen & ~3u) + t; i < wlen; i += 256) db[i] = wg[i];
+  } else {
+    for (uint32_t i = t; i < wlen; i += 256) db[i] = wg[i];
+  }
+  for (uint32_t i = t; i < CL_TABLE / 2; i += 256) reinterpret_cast<uint32_t *>(s->table)[i] = 0xFFFFFFFFu;
+  __syncthreads();
+  auto bucket = [&](uint32_t r) {
+    const uint32_t a = cl_word(s->data, r), b = cl_word(s->data, r + 4);
+    return (a * 0x9E3779B1u ^ b * 0x85EBCA77u) >> (32 - 13);
+  };
+  static_assert(CL_TABLE == 8192, "13-bit buckets");
+  for (uint32_t r = 16 * t; r + 8 <= wlen; r += 16 * 256) s->table[bucket(r)] = (uint16_t)r;
+  __syncthreads();
+  const uint32_t b0 = (uint32_t)((int64_t)lo - h0);  // the block in window coordinates
+  uint32_t hits = 0;
+  for (uint32_t r = b0 + t; r + 8 <= wlen; r += 256) {
+    // (the table keeps one of the equal keys, not always an earlier one:
+    // any other position with the same 8 bytes within a match distance is a
+    // repeat, whichever of the two comes first)
+    const uint32_t q = s->table[bucket(r)];
+    if (q != r && q != 0xFFFFu && (q < r ? r - q : q - r) <= (uint32_t)DF_MAXDIST &&
+        cl_word(s->data, q) == cl_word(s->data, r) && cl_word(s->data, q + 4) == cl_word(s->data, r + 4))
+      ++hits;
+  }
+  for (int off = 32; off; off >>= 1) hits += __shfl_xor(hits, off, 64);
+  if ((t & 63) == 0) s->hits[t >> 6] = hits;
+  __syncthreads();
+  if (t == 0) {
+    const bool st = (s->hits[0] + s->hits[1] + s->hits[2] + s->hits[3]) < CL_HITS;
+    P.store[blk] = st ? 1 : 0;
+    if (st) atomicAdd(P.nstore, 1u);
+  }
 }
 
 // ================================ 1. match_kernel ================================
@@ -596,6 +709,11 @@ __global__ __launch_bounds__(DF_THREADS) void match_kernel(DeflateParams P) {
   if ((wg | 7u) < gridDim.x) wg = (wg & ~7u) | ((wg + (wg >> 3)) & 7u);
   const uint32_t b0 = wg * P.blocks_per_wg;
   const uint32_t b1 = (b0 + P.blocks_per_wg) < P.nblocks ? (b0 + P.blocks_per_wg) : P.nblocks;
+  if (P.store) {  // every block of the super-chunk goes stored: nothing to search
+    bool all = true;
+    for (uint32_t b = b0; b < b1; ++b) all = all && P.store[b];
+    if (all) return;
+  }
   // (batch: a workgroup's blocks belong to one stream, which starts at f_lo)
   const uint64_t f_lo = P.span ? P.halo + P.span[2 * (uint64_t)b0] : 0;
   const uint64_t f_end = P.span ? P.halo + P.span[2 * (uint64_t)b0 + 1] : P.end;
@@ -1239,6 +1357,7 @@ __global__ __launch_bounds__(64) void price_kernel(DeflateParams P) {
   PriceShared *s = &sh;
   const int lane = threadIdx.x;
   const uint32_t blk = blockIdx.x;
+  if (P.store && P.store[blk]) return;  // stored block (classify_kernel)
   const uint64_t lo = (uint64_t)blk * DF_BLOCK;
   const uint64_t n = stream_end(P, blk);
   const uint32_t blen = (uint32_t)((n - lo) < DF_BLOCK ? (n - lo) : DF_BLOCK);
@@ -1290,6 +1409,7 @@ __global__ __launch_bounds__(64) void optparse_kernel(DeflateParams P) {
   OptShared *s = &sh;
   const int lane = threadIdx.x;
   const uint32_t blk = blockIdx.x;
+  if (P.store && P.store[blk]) return;  // stored block (classify_kernel)
   const uint64_t lo = (uint64_t)blk * DF_BLOCK;
   const uint64_t n = stream_end(P, blk);
   const uint32_t blen = (uint32_t)((n - lo) < DF_BLOCK ? (n - lo) : DF_BLOCK);
@@ -1427,6 +1547,7 @@ __global__ __launch_bounds__(64) void parse_kernel(DeflateParams P) {
   PriceShared *s = &sh;
   const int lane = threadIdx.x;
   const uint32_t blk = blockIdx.x;
+  if (P.store && P.store[blk]) return;  // stored block (classify_kernel)
   const uint64_t lo = (uint64_t)blk * DF_BLOCK;
   const uint64_t n = stream_end(P, blk);
   const uint32_t blen = (uint32_t)((n - lo) < DF_BLOCK ? (n - lo) : DF_BLOCK);
@@ -1456,6 +1577,18 @@ __global__ __launch_bounds__(64) void block_kernel(DeflateParams P) {
   const uint32_t blen = (uint32_t)((n - lo) < gspan ? (n - lo) : gspan);
   BlockPlan *plan = P.plans + blk;
   const bool last = P.span ? lo + gspan >= n : P.final_ && (blk + nsub == P.nblocks);
+  if (P.store && P.store[blk]) {  // classify_kernel: bytes that cannot beat a stored block
+    if (lane == 0) {
+      plan->ntok = 0;
+      plan->btype = 0;
+      plan->hdr_bits = 0;
+      plan->hdr_tail = 0;
+      plan->blen = blen;
+      plan->last = last ? 1 : 0;
+      plan->nsub = nsub;
+    }
+    return;
+  }
   // the parse's histograms and token counts (parse_kernel, in each parse
   // block's slot), summed over the group
   uint32_t ntok = 0;
@@ -2084,7 +2217,7 @@ static DeflateLevel level_params(int level) {
 // blocks) align.
 struct DeflateGeom {
   uint32_t nblocks, k, nwg;
-  size_t res_bytes, slot_bytes, len_bytes, off_bytes, plan_bytes;
+  size_t res_bytes, slot_bytes, len_bytes, off_bytes, plan_bytes, store_bytes;
 };
 
 static size_t deflate_geometry(const DeviceCtx *c, size_t n, DeflateGeom *g) {
@@ -2103,7 +2236,8 @@ static size_t deflate_geometry(const DeviceCtx *c, size_t n, DeflateGeom *g) {
   g->len_bytes = ((size_t)g->nblocks * 4 + 255) & ~size_t(255);
   g->off_bytes = ((size_t)(g->nblocks + 1) * 8 + 255) & ~size_t(255);
   g->plan_bytes = ((size_t)g->nblocks * sizeof(BlockPlan) + 255) & ~size_t(255);
-  return g->res_bytes + g->slot_bytes + g->len_bytes + g->off_bytes + g->plan_bytes + 256;
+  g->store_bytes = ((size_t)g->nblocks + 256 + 255) & ~size_t(255);  // flags + the counter
+  return g->res_bytes + g->slot_bytes + g->len_bytes + g->off_bytes + g->plan_bytes + g->store_bytes + 256;
 }
 
 // tuning hook: ZT_DF_RESTART = blocks per independent segment (>= 8, rounded
@@ -2111,6 +2245,14 @@ static size_t deflate_geometry(const DeviceCtx *c, size_t n, DeflateGeom *g) {
 static uint32_t restart_blocks() {
   static const int e = getenv("ZT_DF_RESTART") ? atoi(getenv("ZT_DF_RESTART")) : 0;
   return e >= 4 ? (uint32_t)e : kRestartBlocks;
+}
+
+// classify_kernel runs for the best-of-three block choice (compressionType
+// DYNAMIC) with one parse block per DEFLATE block; ZT_DF_CLASSIFY=0 turns it
+// off (A/B measurement only)
+static bool classify_on(int ctype) {
+  static const bool off = getenv("ZT_DF_CLASSIFY") && atoi(getenv("ZT_DF_CLASSIFY")) == 0;
+  return ctype == 2 && DF_GROUP == 1 && !off;
 }
 
 // bytes per independent segment: a deflate call on a slice that starts at a
@@ -2172,12 +2314,20 @@ int deflate_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t halo, in
   P.ctype = ctype;
   P.opt = L.opt && ctype == 2;
   P.span = nullptr;
+  P.nstore = nullptr;
   P.res = reinterpret_cast<uint32_t *>(sb);
   P.slots = sb + G.res_bytes;
   P.slot_len = reinterpret_cast<uint32_t *>(sb + G.res_bytes + G.slot_bytes);
   uint64_t *off = reinterpret_cast<uint64_t *>(sb + G.res_bytes + G.slot_bytes + G.len_bytes);
   P.plans = reinterpret_cast<BlockPlan *>(sb + G.res_bytes + G.slot_bytes + G.len_bytes + G.off_bytes);
+  P.store = classify_on(ctype) ? sb + G.res_bytes + G.slot_bytes + G.len_bytes + G.off_bytes + G.plan_bytes : nullptr;
   ZT_TRY(timing_begin(c, s, 1));
+  if (P.store) {
+    P.nstore = reinterpret_cast<uint32_t *>(P.store + ((G.nblocks + 255) & ~255u));
+    ZT_HIP(hipMemsetAsync(P.nstore, 0, 4, s));
+    classify_kernel<<<G.nblocks, 256, 0, s>>>(P);
+    ZT_HIP(hipGetLastError());
+  }
   ZT_TRY(timing_begin(c, s, 0));
   match_kernel<<<G.nwg, DF_THREADS, 0, s>>>(P);
   ZT_HIP(hipGetLastError());
@@ -2200,8 +2350,11 @@ int deflate_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t halo, in
   ZT_HIP(hipGetLastError());
   ZT_TRY(timing_end(c, s, 1));
   uint64_t total = 0;
+  uint32_t nstored = 0;
   ZT_HIP(hipMemcpyAsync(&total, off + G.nblocks, sizeof total, hipMemcpyDeviceToHost, s));
+  if (P.store) ZT_HIP(hipMemcpyAsync(&nstored, P.nstore, 4, hipMemcpyDeviceToHost, s));
   ZT_HIP(hipStreamSynchronize(s));
+  c->times.blocks_unsearched += nstored;
   ZT_TRY(timing_collect(c, &c->times.deflate_ms, &c->times.deflate_launches, 0));
   ZT_TRY(timing_collect(c, &c->times.deflate_pipeline_ms, &c->times.deflate_pipelines, 1));
   *out_len = total;
@@ -2266,12 +2419,20 @@ int deflate_batch_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t count, const
   P.ctype = ctype;
   P.opt = L.opt && ctype == 2;
   P.span = d_span;
+  P.nstore = nullptr;
   P.res = reinterpret_cast<uint32_t *>(sb);
   P.slots = sb + G.res_bytes;
   P.slot_len = reinterpret_cast<uint32_t *>(sb + G.res_bytes + G.slot_bytes);
   uint64_t *d_off = reinterpret_cast<uint64_t *>(sb + G.res_bytes + G.slot_bytes + G.len_bytes);
   P.plans = reinterpret_cast<BlockPlan *>(sb + G.res_bytes + G.slot_bytes + G.len_bytes + G.off_bytes);
+  P.store = classify_on(ctype) ? sb + G.res_bytes + G.slot_bytes + G.len_bytes + G.off_bytes + G.plan_bytes : nullptr;
   ZT_TRY(timing_begin(c, s, 1));
+  if (P.store) {
+    P.nstore = reinterpret_cast<uint32_t *>(P.store + ((G.nblocks + 255) & ~255u));
+    ZT_HIP(hipMemsetAsync(P.nstore, 0, 4, s));
+    classify_kernel<<<G.nblocks, 256, 0, s>>>(P);
+    ZT_HIP(hipGetLastError());
+  }
   ZT_TRY(timing_begin(c, s, 0));
   match_kernel<<<G.nblocks, DF_THREADS, 0, s>>>(P);
   ZT_HIP(hipGetLastError());
@@ -2294,8 +2455,11 @@ int deflate_batch_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t count, const
   ZT_HIP(hipGetLastError());
   ZT_TRY(timing_end(c, s, 1));
   std::vector<uint64_t> boff((size_t)G.nblocks + 1);
+  uint32_t nstored = 0;
   ZT_HIP(hipMemcpyAsync(boff.data(), d_off, boff.size() * 8, hipMemcpyDeviceToHost, s));
+  if (P.store) ZT_HIP(hipMemcpyAsync(&nstored, P.nstore, 4, hipMemcpyDeviceToHost, s));
   ZT_HIP(hipStreamSynchronize(s));
+  c->times.blocks_unsearched += nstored;
   ZT_TRY(timing_collect(c, &c->times.deflate_ms, &c->times.deflate_launches, 0));
   ZT_TRY(timing_collect(c, &c->times.deflate_pipeline_ms, &c->times.deflate_pipelines, 1));
   for (size_t f = 0; f < count; ++f) out_off[f] = boff[first[f]];

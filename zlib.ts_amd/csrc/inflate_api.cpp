@@ -72,13 +72,12 @@ static int batch_two_phase(DeviceCtx *c, const uint8_t *d_in, const std::vector<
   });
   const size_t units = ids.size();
   std::vector<TokJob> jobs(units);
-  uint64_t tok_total = 0, in_hi = 0;
+  uint64_t tok_total = 0;
   for (size_t k = 0; k < units; ++k) {
     const size_t i = ids[k];
     TokJob &j = jobs[k];
     j.start = in_off[i] + (index ? index[i] : 0);
     j.end = in_off[i] + n[i];
-    in_hi = std::max<uint64_t>(in_hi, j.end);
     // tokens <= output bytes; every token takes >= 1 input bit
     uint64_t cap = std::max<uint64_t>(65536, 4 * (uint64_t)(n[i] - (index ? index[i] : 0)));
     cap = std::min<uint64_t>(cap, (j.end - j.start) * 8) + 64;

@@ -11,7 +11,8 @@
 //   2. tokenize_kernel: one wave per unit (stream start, or a sync point)
 //      decodes blocks to tokens until it reaches another sync point;
 //      (the candidate list is sorted and deduplicated, and the units' jobs
-//      written, on the device: hipcub radix sort + scan);
+//      written, on the device: rocPRIM radix sort + scans; each unit's token
+//      slot is bounded by the input bits up to the next candidate);
 //   3. the host follows the chain from the stream start (unit -> the sync
 //      point it stopped on -> the unit starting there ...), so sync points
 //      that lie inside data are never used, and cuts the chain into segments
@@ -31,7 +32,8 @@
 #include <cstring>
 #include <vector>
 
-#include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 
 #include "zt_internal.h"
 
@@ -183,29 +185,50 @@ __global__ __launch_bounds__(256) void unit_flags(const uint64_t *__restrict__ k
 }
 
 // unit k + 1 starts at the k-th distinct sync point (unit 0 at `index`);
-// pos[cnt] = the number of distinct sync points
+// pos[cnt] = the number of distinct sync points.  Token slot of a unit: every
+// token takes at least one input bit, and a real unit ends at the next real
+// sync point, so min(cap, 8 x the bytes up to the next candidate + 64)
+// holds it (a false candidate inside a real unit's block can only make that
+// unit overflow its slot: the stream then leaves this path).  Without the
+// bound, every one of a crafted input's dense false candidates took a whole
+// block's slot (~128 KiB each).
 __global__ __launch_bounds__(256) void unit_jobs(const uint64_t *__restrict__ key, const uint32_t *__restrict__ flag,
                                                  const uint32_t *__restrict__ pos, uint32_t cnt, uint64_t n,
                                                  uint64_t index, uint32_t cap, uint64_t *__restrict__ sync,
-                                                 uint8_t *__restrict__ restart, TokJob *__restrict__ jobs) {
+                                                 uint8_t *__restrict__ restart, TokJob *__restrict__ jobs,
+                                                 uint64_t *__restrict__ slot) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  auto job = [&](uint32_t u, uint64_t start) {
+  auto job = [&](uint32_t u, uint64_t start, uint64_t next) {
     TokJob j;
     j.start = start;
-    j.tok_off = (uint64_t)u * cap;
-    const uint64_t left = n - start;
-    j.tok_cap = (uint32_t)(left * 8 + 64 < cap ? left * 8 + 64 : cap);
+    j.tok_off = 0;  // unit_slots
+    const uint64_t room = (next > start ? next - start : 0) * 8 + 64;
+    j.tok_cap = (uint32_t)(room < cap ? room : cap);
     j.stop_first = u;  // sync[u] is the first sync point after start
     j.end = 0;
     jobs[u] = j;
+    slot[u] = (j.tok_cap + 63) & ~63u;
   };
-  if (i == 0) job(0, index);
+  if (i == 0) job(0, index, cnt ? key[0] >> 1 : n);
   if (i >= cnt || !flag[i]) return;
   const uint32_t k = pos[i];
   const uint64_t p = key[i] >> 1;
+  uint32_t j = i + 1;
+  while (j < cnt && (key[j] >> 1) == p) ++j;
   sync[k] = p;
   restart[k] = (uint8_t)(key[i] & 1);
-  job(k + 1, p);
+  job(k + 1, p, j < cnt ? key[j] >> 1 : n);
+}
+
+// token offsets = exclusive scan of the slots; total[0] = all slots
+__global__ __launch_bounds__(256) void unit_slots(const uint64_t *__restrict__ off, const uint64_t *__restrict__ slot,
+                                                  const uint32_t *__restrict__ nunits_m1, TokJob *__restrict__ jobs,
+                                                  uint64_t *__restrict__ total) {
+  const uint32_t u = blockIdx.x * 256 + threadIdx.x;
+  const uint32_t units = *nunits_m1 + 1;
+  if (u >= units) return;
+  jobs[u].tok_off = off[u];
+  if (u + 1 == units) total[0] = off[u] + slot[u];
 }
 
 }  // namespace
@@ -241,29 +264,35 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   IT("sync points counted");
   if (cnt == 0 || cnt > kMaxSync) FALLBACK("%u sync points\n", cnt);
   // 2. the candidates sorted, deduplicated and turned into units on the
-  // device (hipcub radix sort + scan): unit 0 starts at `index`, unit k + 1
+  // device (rocPRIM radix sort + scan): unit 0 starts at `index`, unit k + 1
   // at the k-th sync point
   int end_bit = 1;
   while (end_bit < 64 && ((uint64_t)n << 1 | 1) >> end_bit) ++end_bit;
-  size_t t_sort = 0, t_scan = 0;
-  ZT_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, t_sort, (const uint64_t *)nullptr, (uint64_t *)nullptr,
-                                           (int)cnt, 0, end_bit, s));
-  ZT_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, t_scan, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-                                          (int)cnt + 1, s));
-  const size_t t_bytes = align256(std::max(t_sort, t_scan));
-  const size_t key_bytes = align256((size_t)cnt * 8), flag_bytes = align256(((size_t)cnt + 1) * 4);
+  const size_t units_max = (size_t)cnt + 1;
+  size_t t_sort = 0, t_scan = 0, t_scan64 = 0;
+  ZT_HIP(rocprim::radix_sort_keys(nullptr, t_sort, (const uint64_t *)nullptr, (uint64_t *)nullptr, (size_t)cnt, 0u,
+                                  (unsigned)end_bit, s));
+  ZT_HIP(rocprim::exclusive_scan(nullptr, t_scan, (const uint32_t *)nullptr, (uint32_t *)nullptr, 0u, units_max,
+                                 rocprim::plus<uint32_t>(), s));
+  ZT_HIP(rocprim::exclusive_scan(nullptr, t_scan64, (const uint64_t *)nullptr, (uint64_t *)nullptr, (uint64_t)0,
+                                 units_max, rocprim::plus<uint64_t>(), s));
+  const size_t t_bytes = align256(std::max(t_sort, std::max(t_scan, t_scan64)));
+  const size_t key_bytes = align256((size_t)cnt * 8), flag_bytes = align256(units_max * 4);
+  const size_t slot_bytes = align256(units_max * 8);
   void *d_sort;
-  ZT_TRY(scratch(c, 20, t_bytes + key_bytes + 2 * flag_bytes, &d_sort));
+  ZT_TRY(scratch(c, 20, t_bytes + key_bytes + 2 * flag_bytes + 2 * slot_bytes + 256, &d_sort));
   uint8_t *sb = static_cast<uint8_t *>(d_sort);
   uint64_t *d_key = reinterpret_cast<uint64_t *>(sb + t_bytes);
   uint32_t *d_flag = reinterpret_cast<uint32_t *>(sb + t_bytes + key_bytes);
   uint32_t *d_pos = reinterpret_cast<uint32_t *>(sb + t_bytes + key_bytes + flag_bytes);
-  ZT_HIP(hipcub::DeviceRadixSort::SortKeys(sb, t_sort, d_list, d_key, (int)cnt, 0, end_bit, s));
+  uint64_t *d_slot = reinterpret_cast<uint64_t *>(sb + t_bytes + key_bytes + 2 * flag_bytes);
+  uint64_t *d_off = d_slot + slot_bytes / 8;
+  uint64_t *d_ttot = d_off + slot_bytes / 8;  // [0] token slots in all, [1] distinct sync points
+  ZT_HIP(rocprim::radix_sort_keys(sb, t_sort, d_list, d_key, (size_t)cnt, 0u, (unsigned)end_bit, s));
   const uint32_t g = (cnt + 1 + 255) / 256;
   unit_flags<<<g, 256, 0, s>>>(d_key, cnt, d_flag);
   ZT_HIP(hipGetLastError());
-  ZT_HIP(hipcub::DeviceScan::ExclusiveSum(sb, t_scan, d_flag, d_pos, (int)cnt + 1, s));
-  const size_t units_max = (size_t)cnt + 1;
+  ZT_HIP(rocprim::exclusive_scan(sb, t_scan, d_flag, d_pos, 0u, units_max, rocprim::plus<uint32_t>(), s));
   const size_t stops_bytes = align256((size_t)cnt * 8);
   const size_t restart_bytes = align256(units_max);
   const size_t jobs_bytes = align256(units_max * sizeof(TokJob));
@@ -275,22 +304,25 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   TokJob *d_jobs = reinterpret_cast<TokJob *>(static_cast<uint8_t *>(d_meta) + stops_bytes + restart_bytes);
   TokResult *d_res =
       reinterpret_cast<TokResult *>(static_cast<uint8_t *>(d_meta) + stops_bytes + restart_bytes + jobs_bytes);
-  unit_jobs<<<g, 256, 0, s>>>(d_key, d_flag, d_pos, cnt, n, index, kUnitTokCap, d_stops, d_restart, d_jobs);
+  ZT_HIP(hipMemsetAsync(d_slot, 0, units_max * 8, s));
+  unit_jobs<<<g, 256, 0, s>>>(d_key, d_flag, d_pos, cnt, n, index, kUnitTokCap, d_stops, d_restart, d_jobs, d_slot);
   ZT_HIP(hipGetLastError());
-  uint32_t nsync = 0;
-  ZT_HIP(hipMemcpyAsync(&nsync, d_pos + cnt, 4, hipMemcpyDeviceToHost, s));
+  ZT_HIP(rocprim::exclusive_scan(sb, t_scan64, d_slot, d_off, (uint64_t)0, units_max, rocprim::plus<uint64_t>(), s));
+  unit_slots<<<g, 256, 0, s>>>(d_off, d_slot, d_pos + cnt, d_jobs, d_ttot);
+  ZT_HIP(hipGetLastError());
+  uint64_t tot_h[2] = {0, 0};
+  ZT_HIP(hipMemcpyAsync(&tot_h[0], d_ttot, 8, hipMemcpyDeviceToHost, s));
+  ZT_HIP(hipMemcpyAsync(&tot_h[1], d_pos + cnt, 4, hipMemcpyDeviceToHost, s));
   ZT_HIP(hipStreamSynchronize(s));
   IT("units counted");
+  const uint32_t nsync = (uint32_t)tot_h[1];
   const size_t units = (size_t)nsync + 1;
   // Every candidate sync point gets a token slot before the chain shows which
-  // are real block boundaries, so a stream whose stored data is full of the
-  // pattern (or whose tail holds further members) could ask for far more
-  // than its decode needs: past a budget tied to the input size, or when the
-  // slots cannot be allocated, the stream takes the one-wave path instead.
-  const size_t tok_bytes = (units * (size_t)kUnitTokCap + 256) * 4;  // + slack: chunked token reads
-  // (a highly compressible stream needs far more token bytes than its own
-  // size -- ~4 bytes per output byte -- so the budget is the device's free
-  // memory, not a multiple of the input)
+  // are real block boundaries; the slots are bounded by the input bits up to
+  // the next candidate (unit_jobs), so all of them together stay below 8
+  // tokens per input byte + 64 per candidate.  Past the device's free memory,
+  // or when the slots cannot be allocated, the stream takes the general path.
+  const size_t tok_bytes = ((size_t)tot_h[0] + 256) * 4;  // + slack: chunked token reads
   // (only asked when the cached slots are too small: hipMemGetInfo is a
   // driver round trip on every call otherwise)
   if (tok_bytes > c->buf_size[4]) {
@@ -301,9 +333,9 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   void *d_tok;
   if (scratch(c, 4, tok_bytes, &d_tok) != ZT_OK) FALLBACK("token slots (%zu B) not allocated\n", tok_bytes);
   // metadata comes back through pinned staging (slot 1):
-  // [restart flags | results | chain | segments | statuses]
+  // [restart flags | results | token offsets | chain | segments | statuses]
   void *hp;
-  const size_t meta_a = restart_bytes + res_bytes;
+  const size_t meta_a = restart_bytes + res_bytes + slot_bytes;
   const size_t meta_b = align256(units_max * sizeof(ChainUnit)) + align256(units_max * sizeof(SegJob)) +
                         2 * align256(units_max * 4);
   ZT_TRY(pinned(c, meta_a + meta_b, &hp, 1));
@@ -337,6 +369,8 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   TokResult *res = reinterpret_cast<TokResult *>(pin + restart_bytes);
   ZT_HIP(hipMemcpyAsync(pin, d_restart, nsync, hipMemcpyDeviceToHost, s));
   ZT_HIP(hipMemcpyAsync(res, d_res, units * sizeof(TokResult), hipMemcpyDeviceToHost, s));
+  const uint64_t *tok_off = reinterpret_cast<const uint64_t *>(pin + restart_bytes + res_bytes);
+  ZT_HIP(hipMemcpyAsync(pin + restart_bytes + res_bytes, d_off, units * 8, hipMemcpyDeviceToHost, s));
   ZT_HIP(hipStreamSynchronize(s));
   IT("tokenized");
   if (check) {
@@ -395,7 +429,7 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
       seg_start = total;
       segs.push_back(SegJob{(uint32_t)chain.size(), 0});
     }
-    chain.push_back(ChainUnit{(uint64_t)u * kUnitTokCap, total, seg_start, desc_seg + (total - seg_start), r.ntok,
+    chain.push_back(ChainUnit{tok_off[u], total, seg_start, desc_seg + (total - seg_start), r.ntok,
                               (uint32_t)r.out_len});
     segs.back().count++;
     total += r.out_len;

@@ -291,17 +291,64 @@ int zt_unzip(const uint8_t *in, size_t n, int verify, uint8_t **out, size_t *out
     const size_t m = defl.size();
     // (a member with a known compressed size reads at most 64 KiB past it:
     // a valid stream ends inside, and only a corrupt one would read on into
-    // the next bytes; a member without one -- data descriptor -- reads to
-    // the input's end)
+    // the next bytes.  A member without one -- data descriptor -- is first
+    // bounded by the next local header in file order (or the central
+    // directory) + 64 KiB, so that the batch's per-stream scratch stays
+    // proportional to the archive; only members that fail inside that bound
+    // are decoded again over the rest of the input, as the reference's
+    // RawInflate from the member's offset would read it.)
+    std::vector<size_t> starts;
+    for (uint32_t i = 0; i < total; ++i) starts.push_back(ent[i].local_offset);
+    starts.push_back(cd_off);
+    std::sort(starts.begin(), starts.end());
     std::vector<size_t> in_off(m, 0), nn(m, n), idx(m), bl(m), eip(m);
     std::vector<uint8_t *> bp(m, nullptr);
-    std::vector<int> st(m, 0);
+    // (a batch that fails as a whole -- device memory, HIP -- leaves kNotRun)
+    constexpr int kNotRun = -0x7FFF;
+    std::vector<int> st(m, kNotRun);
+    std::vector<char> bounded(m, 0);
     for (size_t k = 0; k < m; ++k) {
-      idx[k] = std::min(doff[defl[k]], n);
-      nn[k] = open_end[defl[k]] ? n : std::min<size_t>(n, idx[k] + dlen[defl[k]] + (64u << 10));
+      const size_t i = defl[k];
+      idx[k] = std::min(doff[i], n);
+      if (open_end[i]) {
+        const auto nx = std::upper_bound(starts.begin(), starts.end(), (size_t)ent[i].local_offset);
+        if (nx != starts.end() && *nx >= idx[k]) {
+          nn[k] = std::min<size_t>(n, *nx + (64u << 10));
+          bounded[k] = nn[k] < n;
+        }
+      } else {
+        nn[k] = std::min<size_t>(n, idx[k] + dlen[i] + (64u << 10));
+      }
     }
-    (void)inflate_batch_dev_streams(dc, d_in, in_off, nn.data(), idx.data(), m, bp.data(), bl.data(), eip.data(),
-                                    st.data());
+    int rc = inflate_batch_dev_streams(dc, d_in, in_off, nn.data(), idx.data(), m, bp.data(), bl.data(),
+                                       eip.data(), st.data());
+    for (size_t k = 0; k < m; ++k)
+      if (st[k] == kNotRun) return rc ? rc : set_error(ZT_E_INTERNAL, "unzip: member batch not decoded");
+    // members that failed inside their bound: again, to the input's end
+    std::vector<size_t> again;
+    for (size_t k = 0; k < m; ++k)
+      if (st[k] && bounded[k]) again.push_back(k);
+    if (!again.empty()) {
+      const size_t r = again.size();
+      std::vector<size_t> in2(r, 0), nn2(r, n), idx2(r), bl2(r), eip2(r);
+      std::vector<uint8_t *> bp2(r, nullptr);
+      std::vector<int> st2(r, kNotRun);
+      for (size_t j = 0; j < r; ++j) idx2[j] = idx[again[j]];
+      rc = inflate_batch_dev_streams(dc, d_in, in2, nn2.data(), idx2.data(), r, bp2.data(), bl2.data(), eip2.data(),
+                                     st2.data());
+      for (size_t j = 0; j < r; ++j)
+        if (st2[j] == kNotRun) {
+          for (uint8_t *p : bp2) zt_free(p);
+          return rc ? rc : set_error(ZT_E_INTERNAL, "unzip: member batch not decoded");
+        }
+      for (size_t j = 0; j < r; ++j) {
+        const size_t k = again[j];
+        zt_free(bp[k]);
+        bp[k] = bp2[j];
+        bl[k] = bl2[j];
+        st[k] = st2[j];
+      }
+    }
     for (size_t k = 0; k < m; ++k) {
       const size_t i = defl[k];
       if (st[k]) {

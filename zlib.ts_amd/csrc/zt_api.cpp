@@ -540,6 +540,36 @@ int zt_timing_enable(int on) {
   return ZT_OK;
 }
 
+int zt_scratch_bytes(size_t *device_bytes, size_t *pinned_bytes) {
+  DeviceCtx *c;
+  ZT_TRY(get_ctx(&c));
+  std::lock_guard<std::recursive_mutex> ctx_lock(c->mu);
+  size_t d = 0, h = 0;
+  for (size_t v : c->buf_size) d += v;
+  for (size_t v : c->pinned_size) h += v;
+  if (device_bytes) *device_bytes = d;
+  if (pinned_bytes) *pinned_bytes = h;
+  return ZT_OK;
+}
+
+int zt_release_scratch(void) {
+  DeviceCtx *c;
+  ZT_TRY(get_ctx(&c));
+  std::lock_guard<std::recursive_mutex> ctx_lock(c->mu);
+  ZT_HIP(hipDeviceSynchronize());
+  for (int k = 0; k < 22; ++k) {
+    if (c->d_buf[k]) ZT_HIP(hipFree(c->d_buf[k]));
+    c->d_buf[k] = nullptr;
+    c->buf_size[k] = 0;
+  }
+  for (int k = 0; k < 8; ++k) {
+    if (c->h_pinned[k]) ZT_HIP(hipHostFree(c->h_pinned[k]));
+    c->h_pinned[k] = nullptr;
+    c->pinned_size[k] = 0;
+  }
+  return ZT_OK;
+}
+
 int zt_timing_read(zt_kernel_times *out) {
   if (!out) return set_error(ZT_E_ARG, "null output");
   DeviceCtx *c;

@@ -38,7 +38,8 @@ class KernelTimes(ctypes.Structure):
                 ("inflate_ms", ctypes.c_double), ("inflate_launches", ctypes.c_uint64),
                 ("deflate_pipeline_ms", ctypes.c_double), ("deflate_pipelines", ctypes.c_uint64),
                 ("inflate_tok_ms", ctypes.c_double), ("inflate_toks", ctypes.c_uint64),
-                ("inflate_paths", ctypes.c_uint64 * 3), ("general_passes", ctypes.c_uint64)]
+                ("inflate_paths", ctypes.c_uint64 * 3), ("general_passes", ctypes.c_uint64),
+                ("blocks_unsearched", ctypes.c_uint64)]
 
 
 class ZipFile(ctypes.Structure):
@@ -129,6 +130,8 @@ def _load():
         "zt_synth_dev_at": ([ctypes.c_int, u32, ctypes.c_uint64, vp, sz, vp], ctypes.c_int),
         "zt_timing_enable": ([ctypes.c_int], ctypes.c_int),
         "zt_timing_read": ([P(KernelTimes)], ctypes.c_int),
+        "zt_scratch_bytes": ([P(sz), P(sz)], ctypes.c_int),
+        "zt_release_scratch": ([], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name, None)
@@ -150,7 +153,8 @@ SYMBOLS = [
     "zt_crc32_batch", "zt_zip_compress", "zt_unzip", "zt_zlib_compress", "zt_zlib_decompress",
     "zt_dev_checksums", "zt_deflate_plan_create", "zt_deflate_plan_destroy",
     "zt_deflate_bound", "zt_deflate_dev", "zt_inflate_plan_create", "zt_inflate_plan_destroy", "zt_inflate_dev",
-    "zt_synth_dev", "zt_synth_dev_at", "zt_timing_enable", "zt_timing_read",
+    "zt_synth_dev", "zt_synth_dev_at", "zt_timing_enable", "zt_timing_read", "zt_scratch_bytes",
+    "zt_release_scratch",
 ]
 
 
@@ -584,4 +588,16 @@ def timing_read():
             "inflate_ms": t.inflate_ms, "inflate_launches": t.inflate_launches,
             "deflate_pipeline_ms": t.deflate_pipeline_ms, "deflate_pipelines": t.deflate_pipelines,
             "inflate_tok_ms": t.inflate_tok_ms, "inflate_toks": t.inflate_toks,
-            "inflate_paths": list(t.inflate_paths), "general_passes": t.general_passes}
+            "inflate_paths": list(t.inflate_paths), "general_passes": t.general_passes,
+            "blocks_unsearched": t.blocks_unsearched}
+
+
+def scratch_bytes():
+    """(device scratch, pinned host staging) bytes the device context caches."""
+    d, h = ctypes.c_size_t(0), ctypes.c_size_t(0)
+    _check(lib.zt_scratch_bytes(ctypes.byref(d), ctypes.byref(h)))
+    return d.value, h.value
+
+
+def release_scratch():
+    _check(lib.zt_release_scratch())
