@@ -37,6 +37,7 @@
 //      inflate (inflate_seg.hip).
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "zt_internal.h"
@@ -202,32 +203,46 @@ __device__ __forceinline__ uint32_t len_sym(uint32_t L) {  // 0..28 (symbol - 25
 // Blocks that cannot beat a stored block skip the match search and the parse
 // (src/RawDeflate.ts:122-153 is the stored form).  Decided
 // from the block's bytes alone, one 256-thread workgroup per 32 KiB block:
-//  A. order-0 entropy of a 4 KiB sample (16 bytes every blen / 256): below
+//  A. order-0 entropy of a 4 KiB sample (1 KiB at each quarter): below
 //     CL_ENTROPY bits per byte the literals alone would compress -> search;
 //  B. high-entropy blocks are checked for repeats (random data that occurs
 //     twice compresses although its bytes look random): the 8-byte keys of
 //     every 16th position of the window (up to 28 KiB of history in the same
-//     segment + the block) go into an LDS table, every position of the block
-//     looks its key up; a repeat of L bytes gives ~L / 16 hits (the pair's
-//     other position, before or after, within a match distance).  CL_HITS hits
-//     or more -> search.
+//     segment + the block) go into an LDS table (position + a 16-bit
+//     fingerprint per bucket), every position of the block looks its key up
+//     from registers (each thread 128 consecutive positions); a repeat of L
+//     bytes gives ~L / 16 hits (the pair's other position, before or after,
+//     within a match distance).  CL_HITS hits or more -> search.
 // Everything else is flagged: match / price / DP / parse skip the block and
 // block_kernel plans it stored (the smallest form for such bytes: the
 // reference's dynamic block of random data is 0.1 % larger).
 constexpr float CL_ENTROPY = 7.85f;  // uniform bytes: ~7.955 from a 4096-byte sample
 constexpr uint32_t CL_HITS = 8;
 constexpr uint32_t CL_TABLE = 8192;
-constexpr uint32_t CL_WIN = DF_HIST + DF_BLOCK;  // history + block
+constexpr uint32_t CL_EMPTY = 0xFFFFFFFFu;
 struct ClassifyShared {
-  uint32_t data[CL_WIN / 4 + 4];
-  uint16_t table[CL_TABLE];
+  uint32_t table[CL_TABLE];  // window position << 16 | fingerprint
   uint32_t hist[256];
   float part[4];
   uint32_t hits[4];
 };
 
-__device__ __forceinline__ uint32_t cl_word(const uint32_t *w, uint32_t r) {
-  return __builtin_amdgcn_alignbyte(w[(r >> 2) + 1], w[r >> 2], r & 3);
+// 4 stream bytes at g + off (off >= 0 relative to a possibly unaligned g);
+// bytes at or past `end` read as 0
+__device__ __forceinline__ uint32_t cl_gword(const uint8_t *g, int64_t off, uint64_t end) {
+  const uint8_t *a = g + off;
+  if ((reinterpret_cast<uintptr_t>(a) & 3) == 0 && off + 4 <= (int64_t)end)
+    return *reinterpret_cast<const uint32_t *>(a);
+  uint32_t v = 0;
+  for (int k = 0; k < 4; ++k)
+    if (off + k < (int64_t)end) v |= (uint32_t)a[k] << (8 * k);
+  return v;
+}
+// 13-bit bucket and 16-bit fingerprint of an 8-byte key
+__device__ __forceinline__ uint32_t cl_hash(uint32_t a, uint32_t b) {
+  uint32_t h = a * 0x9E3779B1u ^ b * 0x85EBCA77u;
+  h ^= h >> 15;
+  return h * 0x2C1B3C6Du;
 }
 
 __global__ __launch_bounds__(256) void classify_kernel(DeflateParams P) {
@@ -242,12 +257,20 @@ __global__ __launch_bounds__(256) void classify_kernel(DeflateParams P) {
     if (t == 0) P.store[blk] = 0;
     return;
   }
-  // A. entropy of the sample
+  // A. entropy of the sample (4 words every `stride` bytes)
   s->hist[t] = 0;
   __syncthreads();
-  const uint32_t stride = blen / 256;
+  // (four contiguous 1 KiB pieces, a quarter of the block apart: coalesced,
+  // 4 KiB of lines per block instead of one line per sampled word)
+  const uint32_t pstep = (blen / 4) & ~15u;
+  {
+    uint32_t v[4];
+    const uint64_t a = lo + (uint64_t)(t >> 6) * pstep + (t & 63) * 16;
 #pragma unroll
-  for (int j = 0; j < 16; ++j) atomicAdd(&s->hist[g[lo + (uint64_t)t * stride + j]], 1u);
+    for (int j = 0; j < 4; ++j) v[j] = cl_gword(g, (int64_t)(a + 4 * j), n);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) atomicAdd(&s->hist[(v[j >> 2] >> (8 * (j & 3))) & 0xFF], 1u);
+  }
   __syncthreads();
   const float c = (float)s->hist[t];
   float e = c > 0.f ? c * __log2f(c) : 0.f;
@@ -259,43 +282,93 @@ __global__ __launch_bounds__(256) void classify_kernel(DeflateParams P) {
     if (t == 0) P.store[blk] = 0;
     return;
   }
+#ifdef ZT_CL_NOB  // (measurement: stage A alone)
+  if (t == 0) {
+    P.store[blk] = 1;
+    atomicAdd(P.nstore, 1u);
+  }
+  return;
+#endif
   // B. repeats inside the window: history from the block's segment / stream
   const uint64_t f_lo = P.span ? P.span[2 * (uint64_t)blk] : 0;
   const uint64_t seg = ((lo - f_lo) / DF_BLOCK) / P.restart;
-  uint64_t w_lo = f_lo + seg * P.restart * DF_BLOCK;  // segment start (stream coordinates)
+  const uint64_t w_lo = f_lo + seg * P.restart * DF_BLOCK;  // segment start (stream coordinates)
   const bool halo_hist = !P.span && seg == 0 && P.halo > 0;  // the first segment may look into the halo
   int64_t h0 = (int64_t)lo - DF_HIST;
   const int64_t floor_ = halo_hist ? -(int64_t)(P.halo < (uint64_t)DF_HIST ? P.halo : (uint64_t)DF_HIST) : (int64_t)w_lo;
   if (h0 < floor_) h0 = floor_;
   const uint32_t wlen = (uint32_t)((int64_t)lo + blen - h0);
-  const uint8_t *wg = g + h0;
-  uint8_t *db = reinterpret_cast<uint8_t *>(s->data);
-  if ((reinterpret_cast<uintptr_t>(wg) & 3) == 0) {
-    const uint32_t *w32 = reinterpret_cast<const uint32_t *>(wg);
-    for (uint32_t i = t; i < wlen / 4; i += 256) s->data[i] = w32[i];
-    for (uint32_t i = (wlen & ~3u) + t; i < wlen; i += 256) db[i] = wg[i];
-  } else {
-    for (uint32_t i = t; i < wlen; i += 256) db[i] = wg[i];
+  for (uint32_t i = t; i < CL_TABLE; i += 256) s->table[i] = CL_EMPTY;
+  // B1. inserts: every 16th position of the window (at most 15 per thread,
+  // every load issued before the first is used); 8-byte loads when the
+  // stream is 16-byte aligned and the window's reads stay inside it
+  constexpr int NI = (DF_HIST + DF_BLOCK) / (16 * 256);
+  const bool vec = (reinterpret_cast<uintptr_t>(g) & 15) == 0 && (h0 & 15) == 0 && lo + DF_BLOCK + 8 <= n;
+  typedef unsigned int cl_u32x2 __attribute__((ext_vector_type(2)));
+  typedef unsigned int cl_u32x4 __attribute__((ext_vector_type(4)));
+  {
+    uint32_t w[NI][3];
+    const int64_t a4 = h0 & ~int64_t(3);
+    const uint32_t sh = (uint32_t)(h0 - a4);
+    if (vec) {
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const uint32_t r = 16 * (t + 256 * i);
+        const cl_u32x2 v = r + 8 <= wlen ? *reinterpret_cast<const cl_u32x2 *>(g + h0 + r) : cl_u32x2{0, 0};
+        w[i][0] = v.x;
+        w[i][1] = v.y;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const int64_t a = a4 + 16 * (int64_t)(t + 256 * i);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) w[i][j] = cl_gword(g, a + 4 * j, n);
+      }
+    }
+    __syncthreads();  // (the table's EMPTY stores before any insert)
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const uint32_t r = 16 * (t + 256 * i);
+      const uint32_t x0 = vec ? w[i][0] : __builtin_amdgcn_alignbyte(w[i][1], w[i][0], sh);
+      const uint32_t x1 = vec ? w[i][1] : __builtin_amdgcn_alignbyte(w[i][2], w[i][1], sh);
+      const uint32_t hh = cl_hash(x0, x1);
+      if (r + 8 <= wlen) s->table[hh >> 19] = (r << 16) | (hh & 0xFFFFu);
+    }
   }
-  for (uint32_t i = t; i < CL_TABLE / 2; i += 256) reinterpret_cast<uint32_t *>(s->table)[i] = 0xFFFFFFFFu;
   __syncthreads();
-  auto bucket = [&](uint32_t r) {
-    const uint32_t a = cl_word(s->data, r), b = cl_word(s->data, r + 4);
-    return (a * 0x9E3779B1u ^ b * 0x85EBCA77u) >> (32 - 13);
-  };
-  static_assert(CL_TABLE == 8192, "13-bit buckets");
-  for (uint32_t r = 16 * t; r + 8 <= wlen; r += 16 * 256) s->table[bucket(r)] = (uint16_t)r;
-  __syncthreads();
+  // B2. queries: thread t the 128 positions from lo + 128 t (block coordinates k)
   const uint32_t b0 = (uint32_t)((int64_t)lo - h0);  // the block in window coordinates
   uint32_t hits = 0;
-  for (uint32_t r = b0 + t; r + 8 <= wlen; r += 256) {
-    // (the table keeps one of the equal keys, not always an earlier one:
-    // any other position with the same 8 bytes within a match distance is a
-    // repeat, whichever of the two comes first)
-    const uint32_t q = s->table[bucket(r)];
-    if (q != r && q != 0xFFFFu && (q < r ? r - q : q - r) <= (uint32_t)DF_MAXDIST &&
-        cl_word(s->data, q) == cl_word(s->data, r) && cl_word(s->data, q + 4) == cl_word(s->data, r + 4))
-      ++hits;
+  const uint32_t k0 = 128 * t;
+  if (k0 < blen) {
+    uint32_t w[36];
+    if (vec) {
+      const cl_u32x4 *v4 = reinterpret_cast<const cl_u32x4 *>(g + lo + k0);
+#pragma unroll
+      for (int j = 0; j < 9; ++j) {
+        const cl_u32x4 v = v4[j];
+        w[4 * j] = v.x;
+        w[4 * j + 1] = v.y;
+        w[4 * j + 2] = v.z;
+        w[4 * j + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 34; ++j) w[j] = cl_gword(g, (int64_t)(lo + k0 + 4 * j), n);
+    }
+#pragma unroll
+    for (int k = 0; k < 128; ++k) {
+      const uint32_t x0 = (k & 3) ? __builtin_amdgcn_alignbyte(w[(k >> 2) + 1], w[k >> 2], k & 3) : w[k >> 2];
+      const uint32_t x1 =
+          (k & 3) ? __builtin_amdgcn_alignbyte(w[(k >> 2) + 2], w[(k >> 2) + 1], k & 3) : w[(k >> 2) + 1];
+      const uint32_t hh = cl_hash(x0, x1);
+      const uint32_t ent = s->table[hh >> 19];
+      const uint32_t r = b0 + k0 + (uint32_t)k, q = ent >> 16;
+      const bool ok = k0 + (uint32_t)k + 8 <= blen && ent != CL_EMPTY && (ent & 0xFFFFu) == (hh & 0xFFFFu) &&
+                      q != r && (q < r ? r - q : q - r) <= (uint32_t)DF_MAXDIST;
+      hits += ok ? 1u : 0u;
+    }
   }
   for (int off = 32; off; off >>= 1) hits += __shfl_xor(hits, off, 64);
   if ((t & 63) == 0) s->hits[t >> 6] = hits;
@@ -2314,7 +2387,6 @@ int deflate_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t halo, in
   P.ctype = ctype;
   P.opt = L.opt && ctype == 2;
   P.span = nullptr;
-  P.nstore = nullptr;
   P.res = reinterpret_cast<uint32_t *>(sb);
   P.slots = sb + G.res_bytes;
   P.slot_len = reinterpret_cast<uint32_t *>(sb + G.res_bytes + G.slot_bytes);
@@ -2322,9 +2394,10 @@ int deflate_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t halo, in
   P.plans = reinterpret_cast<BlockPlan *>(sb + G.res_bytes + G.slot_bytes + G.len_bytes + G.off_bytes);
   P.store = classify_on(ctype) ? sb + G.res_bytes + G.slot_bytes + G.len_bytes + G.off_bytes + G.plan_bytes : nullptr;
   ZT_TRY(timing_begin(c, s, 1));
+  P.nstore = reinterpret_cast<uint32_t *>(sb + G.res_bytes + G.slot_bytes + G.len_bytes + G.off_bytes +
+                                         G.plan_bytes + ((G.nblocks + 255) & ~255u));
+  ZT_HIP(hipMemsetAsync(P.nstore, 0, 4, s));
   if (P.store) {
-    P.nstore = reinterpret_cast<uint32_t *>(P.store + ((G.nblocks + 255) & ~255u));
-    ZT_HIP(hipMemsetAsync(P.nstore, 0, 4, s));
     classify_kernel<<<G.nblocks, 256, 0, s>>>(P);
     ZT_HIP(hipGetLastError());
   }
@@ -2350,11 +2423,11 @@ int deflate_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t halo, in
   ZT_HIP(hipGetLastError());
   ZT_TRY(timing_end(c, s, 1));
   uint64_t total = 0;
-  uint32_t nstored = 0;
+  uint32_t nst[1] = {0};  // blocks stored unsearched
   ZT_HIP(hipMemcpyAsync(&total, off + G.nblocks, sizeof total, hipMemcpyDeviceToHost, s));
-  if (P.store) ZT_HIP(hipMemcpyAsync(&nstored, P.nstore, 4, hipMemcpyDeviceToHost, s));
+  ZT_HIP(hipMemcpyAsync(nst, P.nstore, 4, hipMemcpyDeviceToHost, s));
   ZT_HIP(hipStreamSynchronize(s));
-  c->times.blocks_unsearched += nstored;
+  c->times.blocks_unsearched += nst[0];
   ZT_TRY(timing_collect(c, &c->times.deflate_ms, &c->times.deflate_launches, 0));
   ZT_TRY(timing_collect(c, &c->times.deflate_pipeline_ms, &c->times.deflate_pipelines, 1));
   *out_len = total;
@@ -2419,7 +2492,6 @@ int deflate_batch_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t count, const
   P.ctype = ctype;
   P.opt = L.opt && ctype == 2;
   P.span = d_span;
-  P.nstore = nullptr;
   P.res = reinterpret_cast<uint32_t *>(sb);
   P.slots = sb + G.res_bytes;
   P.slot_len = reinterpret_cast<uint32_t *>(sb + G.res_bytes + G.slot_bytes);
@@ -2427,9 +2499,10 @@ int deflate_batch_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t count, const
   P.plans = reinterpret_cast<BlockPlan *>(sb + G.res_bytes + G.slot_bytes + G.len_bytes + G.off_bytes);
   P.store = classify_on(ctype) ? sb + G.res_bytes + G.slot_bytes + G.len_bytes + G.off_bytes + G.plan_bytes : nullptr;
   ZT_TRY(timing_begin(c, s, 1));
+  P.nstore = reinterpret_cast<uint32_t *>(sb + G.res_bytes + G.slot_bytes + G.len_bytes + G.off_bytes +
+                                         G.plan_bytes + ((G.nblocks + 255) & ~255u));
+  ZT_HIP(hipMemsetAsync(P.nstore, 0, 4, s));
   if (P.store) {
-    P.nstore = reinterpret_cast<uint32_t *>(P.store + ((G.nblocks + 255) & ~255u));
-    ZT_HIP(hipMemsetAsync(P.nstore, 0, 4, s));
     classify_kernel<<<G.nblocks, 256, 0, s>>>(P);
     ZT_HIP(hipGetLastError());
   }
@@ -2455,11 +2528,11 @@ int deflate_batch_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t count, const
   ZT_HIP(hipGetLastError());
   ZT_TRY(timing_end(c, s, 1));
   std::vector<uint64_t> boff((size_t)G.nblocks + 1);
-  uint32_t nstored = 0;
+  uint32_t nst[1] = {0};  // blocks stored unsearched
   ZT_HIP(hipMemcpyAsync(boff.data(), d_off, boff.size() * 8, hipMemcpyDeviceToHost, s));
-  if (P.store) ZT_HIP(hipMemcpyAsync(&nstored, P.nstore, 4, hipMemcpyDeviceToHost, s));
+  ZT_HIP(hipMemcpyAsync(nst, P.nstore, 4, hipMemcpyDeviceToHost, s));
   ZT_HIP(hipStreamSynchronize(s));
-  c->times.blocks_unsearched += nstored;
+  c->times.blocks_unsearched += nst[0];
   ZT_TRY(timing_collect(c, &c->times.deflate_ms, &c->times.deflate_launches, 0));
   ZT_TRY(timing_collect(c, &c->times.deflate_pipeline_ms, &c->times.deflate_pipelines, 1));
   for (size_t f = 0; f < count; ++f) out_off[f] = boff[first[f]];
