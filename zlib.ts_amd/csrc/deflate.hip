@@ -199,6 +199,18 @@ __device__ __forceinline__ uint32_t len_sym(uint32_t L) {  // 0..28 (symbol - 25
   return 4 * (k - 1) + ((x >> (k - 2)) & 3);
 }
 
+// Per-position match word in res (match_kernel -> price / optparse / parse):
+// the byte at the position in bits 24-31 (so the later kernels never read
+// the input again), the match length (0 or 3..258) in bits 15-23 and its
+// distance (<= DF_MAXDIST < 2^15) in bits 0-14.  optparse_kernel rewrites the
+// length with its choice (0 = literal).
+__device__ __forceinline__ uint32_t res_pack(uint32_t byte, uint32_t len, uint32_t dist) {
+  return (byte << 24) | (len << 15) | dist;
+}
+__device__ __forceinline__ uint32_t res_len(uint32_t r) { return (r >> 15) & 511u; }
+__device__ __forceinline__ uint32_t res_dist(uint32_t r) { return r & 0x7FFFu; }
+__device__ __forceinline__ uint32_t res_byte(uint32_t r) { return r >> 24; }
+
 // ================================ 0. classify_kernel ================================
 // Blocks that cannot beat a stored block skip the match search and the parse
 // (src/RawDeflate.ts:122-153 is the stored form).  Decided
@@ -732,7 +744,7 @@ __device__ __forceinline__ uint32_t walk_finish(const Walk &w, const MatchShared
   carry_len = best_len;
   carry_dist = best_dist;
   if (best_len == 3 && best_dist > (uint32_t)P.too_far) best_len = 0;
-  return best_len >= 3 ? (best_len << 16) | best_dist : 0u;
+  return best_len >= 3 ? res_pack(0, best_len, best_dist) : 0u;
 }
 
 // longest match for positions [pb, pb + 4) of the sub-chunk [p0, p1) -> res_out[p - p0]
@@ -763,6 +775,11 @@ __device__ void search_quad(const MatchShared *s, const DeflateParams &P, uint32
   while (wa.active || wb.active) walk_pair_step(wa, wb, s, P);
   out[1] = walk_finish<1>(wa, s, P, w, nr1, cl, cd);
   out[3] = walk_finish<3>(wb, s, P, w, nr3, cl, cd);
+  // the positions' own bytes (res_pack)
+  out[0] |= win32<16>(w) << 24;
+  out[1] |= win32<17>(w) << 24;
+  out[2] |= win32<18>(w) << 24;
+  out[3] |= win32<19>(w) << 24;
   if (pb + 4 <= p1) {
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     u32x4 v = {out[0], out[1], out[2], out[3]};
@@ -929,10 +946,9 @@ constexpr int PB_CH = 4;
 #define ZT_PB_NCH 4
 #endif
 constexpr int PB_NCH = ZT_PB_NCH;
-constexpr int PB_LOADS = PB_CH + PB_CH / 4;  // global_load_lds per chunk (res words, then data words)
+constexpr int PB_LOADS = PB_CH;  // global_load_lds per chunk (res words; the bytes ride in res)
 struct ParseStage {
   uint32_t res[PB_NCH][PB_CH * 64];
-  uint32_t byt[PB_NCH][PB_CH * 16];
 };
 
 struct BlockShared {
@@ -1185,15 +1201,14 @@ __device__ __forceinline__ void lds_inc(uint32_t *p) {
 // (WRITE = false: histograms of the greedy parse only, res untouched)
 template <bool WRITE, class S>
 __device__ __forceinline__ void parse_window(S *s, const DeflateParams &P, uint32_t *r_blk, uint32_t len, uint32_t w0,
-                                             uint32_t r, uint32_t byte, uint32_t r_next, uint32_t &entry,
-                                             uint32_t &ntok) {
+                                             uint32_t r, uint32_t r_next, uint32_t &entry, uint32_t &ntok) {
   const int lane = threadIdx.x & 63;
     const uint32_t i = w0 + lane;
-    uint32_t L = r >> 16;
+    uint32_t L = res_len(r);
     if (P.lazy && !P.opt) {
       // one-step lazy: a longer match at i + 1 defers this one
-      uint32_t nb = (uint32_t)__shfl_down((int)r, 1, 64) >> 16;
-      const uint32_t first_next = (uint32_t)__shfl((int)r_next, 0, 64) >> 16;
+      uint32_t nb = res_len((uint32_t)__shfl_down((int)r, 1, 64));
+      const uint32_t first_next = res_len((uint32_t)__shfl((int)r_next, 0, 64));
       if (lane == 63) nb = first_next;
       if (L >= 3 && i + 1 < len && nb > L) L = 0;
     }
@@ -1245,14 +1260,14 @@ __device__ __forceinline__ void parse_window(S *s, const DeflateParams &P, uint3
     if (on) {
       uint32_t token;
       if (L >= 3) {
-        token = (L << 16) | (r & 0xFFFF);
+        token = (L << 16) | res_dist(r);
         uint32_t eb, ev;
 #ifndef ZT_EXP_NOHIST
         lds_inc(&s->lit_hist[257 + len_sym(L)]);
-        lds_inc(&s->dist_hist[dist_sym(r & 0xFFFF, eb, ev)]);
+        lds_inc(&s->dist_hist[dist_sym(res_dist(r), eb, ev)]);
 #endif
       } else {
-        token = byte;
+        token = res_byte(r);
 #ifndef ZT_EXP_NOHIST
         lds_inc(&s->lit_hist[token]);
 #endif
@@ -1268,36 +1283,34 @@ __device__ __forceinline__ void parse_window(S *s, const DeflateParams &P, uint3
 // register-prefetch driver (any alignment / length)
 constexpr int PB_PF = 6;  // parse windows prefetched
 template <bool WRITE, class S>
-__device__ uint32_t parse_block_regs(S *s, const DeflateParams &P, uint32_t *r_blk, const uint8_t *data, uint32_t len) {
+__device__ uint32_t parse_block_regs(S *s, const DeflateParams &P, uint32_t *r_blk, uint32_t len) {
   const int lane = threadIdx.x & 63;
   uint32_t entry = 0;  // first path position relative to the current window
   uint32_t ntok = 0;
   // software pipeline: PB_PF windows' loads are in flight while one is parsed
-  // (rq[j] / bq[j] hold window w0 + 64 j; rq[j + 1] is the lazy look-ahead)
-  uint32_t rq[PB_PF], bq[PB_PF];
+  // (rq[j] holds window w0 + 64 j; rq[j + 1] is the lazy look-ahead)
+  uint32_t rq[PB_PF];
 #pragma unroll
   for (int j = 0; j < PB_PF; ++j) {
     const uint32_t p = 64u * j + lane;
     rq[j] = p < len ? r_blk[p] : 0u;
-    bq[j] = p < len ? data[p] : 0u;
   }
   for (uint32_t wb = 0; wb < len; wb += 64 * PB_PF) {
 #pragma unroll
     for (int j = 0; j < PB_PF; ++j) {
       const uint32_t w0 = wb + 64u * j;
       if (w0 >= len) break;
-      const uint32_t r = rq[j], byte = bq[j];
+      const uint32_t r = rq[j];
       {
         const uint32_t p = w0 + 64u * PB_PF + lane;
         rq[j] = p < len ? r_blk[p] : 0u;
-        bq[j] = p < len ? data[p] : 0u;
       }
       const uint32_t r_next = rq[(j + 1) % PB_PF];
       if (entry >= 64) {
         entry -= 64;
         continue;
       }
-      parse_window<WRITE>(s, P, r_blk, len, w0, r, byte, r_next, entry, ntok);
+      parse_window<WRITE>(s, P, r_blk, len, w0, r, r_next, entry, ntok);
     }
   }
   return ntok;
@@ -1316,8 +1329,7 @@ __device__ __forceinline__ void vm_wait_loads(void) {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0F70);
 }
 template <bool WRITE, class S>
-__device__ uint32_t parse_block_dma(S *s, ParseStage *st, const DeflateParams &P, uint32_t *r_blk, const uint8_t *data,
-                                    uint32_t len) {
+__device__ uint32_t parse_block_dma(S *s, ParseStage *st, const DeflateParams &P, uint32_t *r_blk, uint32_t len) {
   const int lane = threadIdx.x & 63;
   const uint32_t nch = len / (PB_CH * 64);  // len: a multiple of PB_CH * 64
   auto issue = [&](uint32_t c) {
@@ -1327,10 +1339,6 @@ __device__ uint32_t parse_block_dma(S *s, ParseStage *st, const DeflateParams &P
 #pragma unroll
     for (int w = 0; w < PB_CH; ++w)
       __builtin_amdgcn_global_load_lds(r_blk + cc * (PB_CH * 64) + w * 64 + lane, &st->res[slot][w * 64], 4, 0, 0);
-#pragma unroll
-    for (int w = 0; w < PB_CH / 4; ++w)
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint32_t *>(data + cc * (PB_CH * 64) + w * 256) + lane,
-                                       &st->byt[slot][w * 64], 4, 0, 0);
   };
 #pragma unroll
   for (int c = 0; c < PB_NCH - 1; ++c) issue((uint32_t)c);
@@ -1339,7 +1347,6 @@ __device__ uint32_t parse_block_dma(S *s, ParseStage *st, const DeflateParams &P
     issue(c + PB_NCH - 1);
     vm_wait_loads();
     const uint32_t slot = c % PB_NCH, nslot = (c + 1) % PB_NCH;
-    const uint8_t *bytes = reinterpret_cast<const uint8_t *>(st->byt[slot]);
     for (int w = 0; w < PB_CH; ++w) {
       const uint32_t w0 = c * (PB_CH * 64) + (uint32_t)w * 64;
       if (entry >= 64) {
@@ -1347,9 +1354,8 @@ __device__ uint32_t parse_block_dma(S *s, ParseStage *st, const DeflateParams &P
         continue;
       }
       const uint32_t r = st->res[slot][w * 64 + lane];
-      const uint32_t byte = bytes[w * 64 + lane];
       const uint32_t r_next = w + 1 < PB_CH ? st->res[slot][(w + 1) * 64] : st->res[nslot][0];
-      parse_window<WRITE>(s, P, r_blk, len, w0, r, byte, r_next, entry, ntok);
+      parse_window<WRITE>(s, P, r_blk, len, w0, r, r_next, entry, ntok);
     }
   }
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): no DMA into the ring after return
@@ -1357,11 +1363,9 @@ __device__ uint32_t parse_block_dma(S *s, ParseStage *st, const DeflateParams &P
 }
 
 template <bool WRITE, class S>
-__device__ uint32_t parse_block(S *s, ParseStage *st, const DeflateParams &P, uint32_t *r_blk, const uint8_t *data,
-                                uint32_t len) {
-  if (len % (PB_CH * 64) == 0 && len > 0 && (reinterpret_cast<uintptr_t>(data) & 3) == 0)
-    return parse_block_dma<WRITE>(s, st, P, r_blk, data, len);
-  return parse_block_regs<WRITE>(s, P, r_blk, data, len);
+__device__ uint32_t parse_block(S *s, ParseStage *st, const DeflateParams &P, uint32_t *r_blk, uint32_t len) {
+  if (len % (PB_CH * 64) == 0 && len > 0) return parse_block_dma<WRITE>(s, st, P, r_blk, len);
+  return parse_block_regs<WRITE>(s, P, r_blk, len);
 }
 
 // ================================ 1b. optparse_kernel ================================
@@ -1395,9 +1399,10 @@ constexpr int OP_OV = 128;
 constexpr int OP_RING = ZT_OP_RING;
 constexpr int OP_SHORT = 16;
 #ifndef ZT_OP_PF
-#define ZT_OP_PF 3
+#define ZT_OP_PF 1
 #endif
-constexpr int OP_PF = ZT_OP_PF;      // groups of 16 positions prefetched per lane  // every cut length 3..OP_SHORT is tried, longer ones only at L
+constexpr int OP_PF = ZT_OP_PF;
+constexpr int OP_G = 32;  // positions per group (one 128-byte line of res)      // groups of 16 positions prefetched per lane  // every cut length 3..OP_SHORT is tried, longer ones only at L
 
 // prices of one block, in 1/8 bits (price_kernel -> optparse_kernel), kept at
 // the start of the block's slot until block_kernel writes its header there
@@ -1440,7 +1445,7 @@ __global__ __launch_bounds__(64) void price_kernel(DeflateParams P) {
   // the prices only need symbol statistics: a greedy parse of the block's
   // first 1/ZT_PRICE_SAMPLE (the full block when smaller) estimates them
   const uint32_t plen = blen < (uint32_t)(DF_BLOCK / ZT_PRICE_SAMPLE) ? blen : (uint32_t)(DF_BLOCK / ZT_PRICE_SAMPLE);
-  parse_block<false>(s, &s->stage, P, P.res + lo, P.base + P.halo + lo, plen);
+  parse_block<false>(s, &s->stage, P, P.res + lo, plen);
   wsync();
   BlockPrices *bp = reinterpret_cast<BlockPrices *>(P.slots + (size_t)blk * DF_SLOT);
   float tl = 0.f, td = 0.f;
@@ -1477,7 +1482,10 @@ __device__ __forceinline__ uint32_t op_min3(uint32_t a, uint32_t b, uint32_t c) 
   return r;
 }
 
-__global__ __launch_bounds__(64) void optparse_kernel(DeflateParams P) {
+#ifndef ZT_OP_MINW
+#define ZT_OP_MINW 4  // waves per SIMD the register budget must allow (128 VGPRs)
+#endif
+__global__ __launch_bounds__(64, ZT_OP_MINW) void optparse_kernel(DeflateParams P) {
   __shared__ OptShared sh;
   OptShared *s = &sh;
   const int lane = threadIdx.x;
@@ -1486,7 +1494,6 @@ __global__ __launch_bounds__(64) void optparse_kernel(DeflateParams P) {
   const uint64_t lo = (uint64_t)blk * DF_BLOCK;
   const uint64_t n = stream_end(P, blk);
   const uint32_t blen = (uint32_t)((n - lo) < DF_BLOCK ? (n - lo) : DF_BLOCK);
-  const uint8_t *data = P.base + P.halo + lo;
   uint32_t *r_blk = P.res + lo;
   const BlockPrices *bp = reinterpret_cast<const BlockPrices *>(P.slots + (size_t)blk * DF_SLOT);
   if (bp->any_match == 0) return;  // no match anywhere: the greedy parse is all literals already
@@ -1512,51 +1519,41 @@ __global__ __launch_bounds__(64) void optparse_kernel(DeflateParams P) {
     uint32_t cr9[OP_SHORT + 1];  // cr9[l] = C[i + l] << 9 (0 past the segment's end)
 #pragma unroll
     for (int l = 0; l <= OP_SHORT; ++l) cr9[l] = 0;
-    const uint32_t g_last = (e - 1) & ~15u;
-    const uint32_t ngroups = (g_last - s0) / 16 + 1;
-    const bool d_aligned = (reinterpret_cast<uintptr_t>(data) & 3) == 0;
-    // a group is 16 positions: 64 bytes of res and 16 data bytes per lane, so
-    // the 64 lanes' scattered reads still use whole cache lines
-    auto load_g = [&](uint32_t g, op_u32x4 *r4, op_u32x4 &b4) {
+    const uint32_t g_last = (e - 1) & ~uint32_t(OP_G - 1);
+    const uint32_t ngroups = (g_last - s0) / OP_G + 1;
+    // a group is OP_G = 32 positions: one whole 128-byte line of res per
+    // lane (the literal's byte rides in res), so the 64 lanes' scattered
+    // reads each use the full line they fetch (16-position groups read half
+    // lines + 16 data bytes: 13.4 GB of reads per GiB, profiles/r04pmc_*)
+    auto load_g = [&](uint32_t g, op_u32x4 *r4) {
       const op_u32x4 *src = reinterpret_cast<const op_u32x4 *>(r_blk + g);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) r4[q] = src[q];
-      if (d_aligned && g + 15 < blen) {
-        const uint32_t *d4 = reinterpret_cast<const uint32_t *>(data + g);
-        b4 = op_u32x4{d4[0], d4[1], d4[2], d4[3]};
-      } else {
-        uint32_t w[4] = {0, 0, 0, 0};
-        for (int k = 0; k < 16; ++k)
-          if (g + k < blen) w[k >> 2] |= (uint32_t)data[g + k] << (8 * (k & 3));
-        b4 = op_u32x4{w[0], w[1], w[2], w[3]};
-      }
+      for (int q = 0; q < OP_G / 4; ++q) r4[q] = src[q];
     };
-    // OP_PF groups in flight per lane: HBM latency is hidden by depth (one
-    // wave per SIMD here)
-    op_u32x4 rq[OP_PF][4];
-    op_u32x4 bq[OP_PF];
+    // OP_PF groups in flight per lane: HBM latency is hidden by depth
+    op_u32x4 rq[OP_PF][OP_G / 4];
 #pragma unroll
     for (int j = 0; j < OP_PF; ++j)
-      if ((uint32_t)j < ngroups) load_g(g_last - 16u * (uint32_t)j, rq[j], bq[j]);
+      if ((uint32_t)j < ngroups) load_g(g_last - (uint32_t)OP_G * (uint32_t)j, rq[j]);
     uint32_t gi = 0;  // groups done
     while (gi < ngroups) {
 #pragma unroll
       for (int j = 0; j < OP_PF; ++j) {
         if (gi < ngroups) {
-          const uint32_t g = g_last - 16u * gi;
-          op_u32x4 rv[4] = {rq[j][0], rq[j][1], rq[j][2], rq[j][3]};
-          const op_u32x4 bv4 = bq[j];
-          if (gi + OP_PF < ngroups) load_g(g - 16u * OP_PF, rq[j], bq[j]);
+          const uint32_t g = g_last - (uint32_t)OP_G * gi;
+          op_u32x4 rv[OP_G / 4];
 #pragma unroll
-          for (int k = 15; k >= 0; --k) {
+          for (int q = 0; q < OP_G / 4; ++q) rv[q] = rq[j][q];
+          if (gi + OP_PF < ngroups) load_g(g - (uint32_t)OP_G * OP_PF, rq[j]);
+#pragma unroll
+          for (int k = OP_G - 1; k >= 0; --k) {
             // positions >= e (the tail of the block's last group) are steps
             // with price 0 and no match: C stays 0 there, as past the end
             const uint32_t i = g + (uint32_t)k;
             const bool live = i < e;
             {
               const uint32_t r = rv[k >> 2][k & 3];
-              const uint32_t L = live ? r >> 16 : 0u, D = r & 0xFFFF;
-              const uint32_t bv = bv4[k >> 2];
+              const uint32_t L = live ? res_len(r) : 0u, D = res_dist(r);
               // C[i+1 .. i+OP_SHORT] live in registers (cr[1..]); only the
               // full-length candidate reads the LDS ring.  Candidates are
               // compared as keys (price relative to C[i+1], biased) << 9 | l.
@@ -1567,7 +1564,7 @@ __global__ __launch_bounds__(64) void optparse_kernel(DeflateParams P) {
               const uint32_t Lr = Lc < (uint32_t)OP_RING ? Lc : (uint32_t)OP_RING;
               const uint32_t rr = row >= Lr ? row - Lr : row + OP_RING - Lr;
               const int c_far = (int)(int16_t)(uint16_t)(s->ring[rr][lane] - (uint16_t)C1) + (int)s->pr.lenc[Lc];
-              const int lit = live ? (int)s->pr.litc[(bv >> (8 * (k & 3))) & 0xFF] : 0;
+              const int lit = live ? (int)s->pr.litc[res_byte(r)] : 0;
               uint32_t key = (uint32_t)(lit + 0x8000) << 9;
               // key of length l: (price + C[i+l] - C[i+1] + bias) << 9 | l,
               // one add3 of pre-shifted terms (exact modulo 2^32: the
@@ -1590,7 +1587,7 @@ __global__ __launch_bounds__(64) void optparse_kernel(DeflateParams P) {
 #pragma unroll
               for (int l = OP_SHORT; l > 1; --l) cr9[l] = cr9[l - 1];
               cr9[1] = C1 << 9;
-              rv[k >> 2][k & 3] = choice ? (choice << 16) | D : 0u;
+              rv[k >> 2][k & 3] = (r & 0xFF000000u) | (choice << 15) | D;
             }
           }
           // the group's choices in whole-line stores (positions >= seg_end
@@ -1599,7 +1596,7 @@ __global__ __launch_bounds__(64) void optparse_kernel(DeflateParams P) {
           if (g < seg_end) {
             op_u32x4 *dst = reinterpret_cast<op_u32x4 *>(r_blk + g);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) dst[q] = rv[q];
+            for (int q = 0; q < OP_G / 4; ++q) dst[q] = rv[q];
           }
           ++gi;
         }
@@ -1627,7 +1624,7 @@ __global__ __launch_bounds__(64) void parse_kernel(DeflateParams P) {
   for (int i = lane; i < 288; i += 64) s->lit_hist[i] = 0;
   if (lane < 32) s->dist_hist[lane] = 0;
   wsync();
-  const uint32_t ntok = parse_block<true>(s, &s->stage, P, P.res + lo, P.base + P.halo + lo, blen);
+  const uint32_t ntok = parse_block<true>(s, &s->stage, P, P.res + lo, blen);
   wsync();
   uint32_t *hs = reinterpret_cast<uint32_t *>(P.slots + (size_t)blk * DF_SLOT);
   for (int i = lane; i < 288; i += 64) hs[i] = s->lit_hist[i];
