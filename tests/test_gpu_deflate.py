@@ -260,3 +260,29 @@ def test_output_does_not_depend_on_the_run(zt, oracle, level):
         zt.deflate_raw(oracle.gen("wordsalad", 100 + seed, 4 << 20), level=1)
         assert zt.deflate_raw(data, level=level) == first
     check_stream(oracle, zt, data, first)
+
+
+@pytest.mark.parametrize("shift", [1, 2, 3])
+def test_device_stream_at_unaligned_output(zt, oracle, shift):
+    """encode_kernel writes every block straight into the stream at its
+    scanned offset, sharing boundary words with its neighbours (byte-masked
+    stores): the stream written at d_out + 1 / 2 / 3 equals the aligned one,
+    for dynamic, fixed-by-size and stored blocks, restart markers included."""
+    import torch
+
+    d = oracle.gen("wordsalad", 31, 5 << 20) + oracle.gen("xorshift32", 31, 1 << 20) + \
+        oracle.gen("structured", 31, (3 << 20) + 777)
+    n = len(d)
+    d_in = torch.frombuffer(bytearray(d), dtype=torch.uint8).cuda()
+    dp = zt.DeflatePlan(n, level=6)
+    d_a = torch.zeros(zt.deflate_bound(n) + 16, dtype=torch.uint8, device="cuda")
+    la = dp.run(d_in.data_ptr(), n, d_a.data_ptr())
+    d_u = torch.full((zt.deflate_bound(n) + 16,), 0xA5, dtype=torch.uint8, device="cuda")
+    lu = dp.run(d_in.data_ptr(), n, d_u.data_ptr() + shift)
+    dp.close()
+    torch.cuda.synchronize()
+    a = d_a[:la].cpu().numpy().tobytes()
+    u = d_u.cpu().numpy().tobytes()
+    assert la == lu and u[shift:shift + lu] == a
+    assert u[:shift] == b"\xa5" * shift and u[shift + lu] == 0xA5  # neighbours untouched
+    assert zlib.decompress(a, -15) == d

@@ -31,8 +31,8 @@
 //   4. encode_kernel -- 512 threads per block: prefix sum of per-thread bit
 //      counts, word-parallel packing; every block ends byte-aligned with an
 //      empty stored block (00 00 FF FF) so blocks concatenate bytewise.
-//   5. scan_sizes + gather_blocks -- exclusive scan of block sizes and a
-//      byte-exact gather into the output stream; 1 MiB segment boundaries
+//   5. scan_sizes (before encode_kernel: block_kernel plans every block's
+//      exact size) places each block, encode_kernel writes it there; 1 MiB segment boundaries
 //      get a restart marker (two empty stored blocks) for segment-parallel
 //      inflate (inflate_seg.hip).
 #include <cstdio>
@@ -74,7 +74,12 @@ constexpr int DF_GROUP = ZT_DF_GROUP;
 static_assert(DF_GROUP >= 1 && DF_GROUP <= 8 && (32 % DF_GROUP) == 0, "group divides a segment");
 constexpr int DF_SUB = 4096;
 constexpr int DF_RING = 32768;  // power of two: ring index = rel & (DF_RING - 1)
-constexpr int DF_SLOT = DF_BLOCK + DF_BLOCK / 8 + 1024;  // per-block slot: fits a forced fixed-code block
+// per-block slot: the block's prices (price_kernel -> optparse_kernel), then
+// its histograms and token count (parse_kernel -> block_kernel), then its
+// dynamic header's complete words (block_kernel -> encode_kernel: at most
+// 17 + 19 * 3 + 316 * 14 bits); the coded block itself goes straight into the stream
+constexpr int DF_SLOT = 2048;
+static_assert(DF_SLOT >= 321 * 4 && DF_SLOT * 8 >= 17 + 19 * 3 + 316 * 14, "slot holds histograms and a header");
 // hash buckets of the 8-byte-key chains (u32 heads) and of the 4-byte-key
 // table (u32 heads, no chains): the sizes fill the 160 KiB of LDS next to the
 // ring, the chain links and the sub-chunk's 4-byte links
@@ -94,7 +99,15 @@ constexpr int DF_THREADS = 1024;
 // the ring holds [p1 - DF_RING, p1) while sub-chunk [p0, p1) is searched;
 // a super-chunk loads DF_HIST bytes of history first (whole sub-chunks)
 constexpr int DF_HIST = DF_RING - DF_SUB;     // 28672
-constexpr int DF_MAXDIST = DF_HIST - 64;      // 28608
+// The first DF_HEAD bytes of the next sub-chunk are in the ring while a
+// sub-chunk is searched, so matches run on past its end (to the block's);
+// they take the ring slots of the window's oldest DF_HEAD - 64 bytes.
+#ifndef ZT_DF_HEAD
+#define ZT_DF_HEAD 320
+#endif
+constexpr int DF_HEAD = ZT_DF_HEAD;
+static_assert(DF_HEAD == 0 || DF_HEAD >= 258 + 8 + 54, "a head covers a whole match past the sub-chunk end");
+constexpr int DF_MAXDIST = DF_HIST - 64 - (DF_HEAD ? DF_HEAD - 64 : 0);  // 28352 (28608 without heads)
 #ifndef ZT_ENC_THREADS
 #define ZT_ENC_THREADS 512  // 128 / 256 / 512 / 1024: 1.70 / 1.42 / 1.38 / 1.75 ms per GiB (profiles/r02q_encode_variants.txt)
 #endif
@@ -134,8 +147,11 @@ struct DeflateParams {
   uint8_t *store;
   uint32_t *nstore;     // blocks flagged (one counter, zeroed before classify_kernel)
   uint32_t *res;        // n: per-position match, then (in place) per-block tokens
-  uint8_t *slots;       // nblocks x DF_SLOT
-  uint32_t *slot_len;   // nblocks
+  uint8_t *slots;       // nblocks x DF_SLOT (prices, histograms, dynamic headers)
+  uint32_t *slot_len;   // nblocks: each block's bytes (block_kernel's plan, exact)
+  uint8_t *out;         // the stream: encode_kernel writes block b at out + boff[b]
+  const uint64_t *boff; // exclusive scan of slot_len (+ restart markers), scan_sizes
+  uint32_t *fault;      // encode_kernel: a block's bits differ from its plan
   BlockPlan *plans;     // nblocks
 };
 
@@ -715,8 +731,8 @@ __device__ __forceinline__ void walk_pair_step(Walk &a, Walk &b, const MatchShar
 // that make up much of source text)
 template <int K>
 __device__ __forceinline__ uint32_t walk_finish(const Walk &w, const MatchShared *s, const DeflateParams &P,
-                                                const uint32_t (&win)[9], uint32_t near, uint32_t &carry_len,
-                                                uint32_t &carry_dist) {
+                                                const uint32_t (&win)[9], uint32_t near, uint32_t lim4,
+                                                uint32_t &carry_len, uint32_t &carry_dist) {
   uint32_t best_len = w.best_len < w.cl ? w.cl : w.best_len, best_dist = w.best_dist;
   // a far 3-byte match (carried from the previous position) is dropped in
   // the end: it must not hide a near one
@@ -725,7 +741,9 @@ __device__ __forceinline__ uint32_t walk_finish(const Walk &w, const MatchShared
   if (near == 0 && w.max_len >= 3 && short_)
     near_probe<K, 1>(win, w.cur, w.cur2, w.p, w.max_len, P.probe, best_len, best_dist);
 #ifndef ZT_DF_NOP4
-  if (w.max_len >= 4 && short_) {
+  // (positions from lim4 on have no 4-byte link: their keys would need bytes
+  // past the segment's end)
+  if (w.max_len >= 4 && short_ && w.p < lim4) {
     const uint32_t d4 = s->link4[w.p & (DF_SUB - 1)];
     uint32_t qw[2];
     ld_run<2>(s, w.p - d4, qw);
@@ -747,9 +765,10 @@ __device__ __forceinline__ uint32_t walk_finish(const Walk &w, const MatchShared
   return best_len >= 3 ? res_pack(0, best_len, best_dist) : 0u;
 }
 
-// longest match for positions [pb, pb + 4) of the sub-chunk [p0, p1) -> res_out[p - p0]
+// longest match for positions [pb, pb + 4) of the sub-chunk [p0, p1) -> res_out[p - p0];
+// matches end at pml (>= p1)
 __device__ void search_quad(const MatchShared *s, const DeflateParams &P, uint32_t pb, uint32_t p0, uint32_t p1,
-                            Key key, uint32_t *res_out) {
+                            uint32_t pml, uint32_t lim4, Key key, uint32_t *res_out) {
   if (pb >= p1) return;
   // bytes [pb - 16, pb + 20) (pb is a multiple of 4; before rel 0 the words
   // are never used: near distances stay <= p)
@@ -762,19 +781,19 @@ __device__ void search_quad(const MatchShared *s, const DeflateParams &P, uint32
   const uint32_t nr0 = near_any<0, 1>(w, win32<16>(w), ~0u), nr1 = near_any<1, 1>(w, win32<17>(w), ~0u);
   const uint32_t nr2 = near_any<2, 1>(w, win32<18>(w), ~0u), nr3 = near_any<3, 1>(w, win32<19>(w), ~0u);
   Walk wa, wb;
-  walk_init(wa, s, P, pb, p1, win32<16>(w), win32<20>(w), win32<24>(w), win32<28>(w), 0, 0);
-  walk_init(wb, s, P, pb + 2, p1, win32<18>(w), win32<22>(w), win32<26>(w), win32<30>(w), 0, 0);
+  walk_init(wa, s, P, pb, pml, win32<16>(w), win32<20>(w), win32<24>(w), win32<28>(w), 0, 0);
+  walk_init(wb, s, P, pb + 2, pml, win32<18>(w), win32<22>(w), win32<26>(w), win32<30>(w), 0, 0);
   while (wa.active || wb.active) walk_pair_step(wa, wb, s, P);
-  out[0] = walk_finish<0>(wa, s, P, w, nr0, c0l, c0d);
-  out[2] = walk_finish<2>(wb, s, P, w, nr2, c2l, c2d);
+  out[0] = walk_finish<0>(wa, s, P, w, nr0, lim4, c0l, c0d);
+  out[2] = walk_finish<2>(wb, s, P, w, nr2, lim4, c2l, c2d);
 #ifdef ZT_DF_NOCARRY  // experiment: positions 1 and 3 start without the carried match
   c0l = c0d = c2l = c2d = 0;
 #endif
-  walk_init(wa, s, P, pb + 1, p1, win32<17>(w), win32<21>(w), win32<25>(w), win32<29>(w), c0l, c0d);
-  walk_init(wb, s, P, pb + 3, p1, win32<19>(w), win32<23>(w), win32<27>(w), win32<31>(w), c2l, c2d);
+  walk_init(wa, s, P, pb + 1, pml, win32<17>(w), win32<21>(w), win32<25>(w), win32<29>(w), c0l, c0d);
+  walk_init(wb, s, P, pb + 3, pml, win32<19>(w), win32<23>(w), win32<27>(w), win32<31>(w), c2l, c2d);
   while (wa.active || wb.active) walk_pair_step(wa, wb, s, P);
-  out[1] = walk_finish<1>(wa, s, P, w, nr1, cl, cd);
-  out[3] = walk_finish<3>(wb, s, P, w, nr3, cl, cd);
+  out[1] = walk_finish<1>(wa, s, P, w, nr1, lim4, cl, cd);
+  out[3] = walk_finish<3>(wb, s, P, w, nr3, lim4, cl, cd);
   // the positions' own bytes (res_pack)
   out[0] |= win32<16>(w) << 24;
   out[1] |= win32<17>(w) << 24;
@@ -819,7 +838,13 @@ __global__ __launch_bounds__(DF_THREADS) void match_kernel(DeflateParams P) {
   const uint64_t h_lo = s_lo - hist;
   const uint8_t *g = P.base + h_lo;  // rel 0
   const uint32_t rs = (uint32_t)(s_lo - h_lo), re = (uint32_t)(s_hi - h_lo);
-  const uint32_t rend = (uint32_t)(f_end - h_lo);  // bytes available (for hashing)
+  // bytes available for hashing: the stream's, but not past the end of the
+  // super-chunk's segment (a restart point): positions near a segment end
+  // are never linked, so a segment is searched alike whether the stream goes
+  // on or ends there (a shard, a pipeline piece, zt_shard.py)
+  const bool seg_end = s_hi == f_end || (P.span ? ((s_hi - f_lo) / DF_BLOCK) % P.restart == 0
+                                                 : ((s_hi - P.halo) / DF_BLOCK) % P.restart == 0);
+  const uint32_t rend = seg_end ? (uint32_t)(s_hi - h_lo) : (uint32_t)(f_end - h_lo);
   Key key;
   key.kmask = P.klen >= 4 ? 0xFFFFFFFFu : 0xFFFFFFu;
   key.kmask2 = P.klen >= 8 ? 0xFFFFFFFFu : P.klen == 6 ? 0xFFFFu : P.klen == 5 ? 0xFFu : 0u;
@@ -834,13 +859,25 @@ __global__ __launch_bounds__(DF_THREADS) void match_kernel(DeflateParams P) {
   __syncthreads();
   uint32_t inserted = 0;  // positions [0, inserted) are in the chains
   if (re > 0) load_sub(&s, g, 0, re < DF_SUB ? re : DF_SUB);
+  // (the second sub-chunk's head: bytes [DF_SUB, DF_SUB + DF_HEAD); heads
+  // run on past the super-chunk into the stream, so that a position at a
+  // block end is linked and searched alike whatever the super-chunk size)
+  if (DF_HEAD && t < (uint32_t)DF_HEAD && DF_SUB + t < rend) {
+    uint8_t *rb = reinterpret_cast<uint8_t *>(s.ring);
+    const uint8_t b = g[DF_SUB + t];
+    rb[ridx(DF_SUB + t)] = b;
+    if (ridx(DF_SUB + t) < 64) rb[DF_RING + ridx(DF_SUB + t)] = b;
+  }
   const bool g_aligned = (reinterpret_cast<uintptr_t>(g) & 3) == 0;
   for (uint32_t p0 = 0; p0 < re; p0 += DF_SUB) {
     const uint32_t p1 = (p0 + DF_SUB) < re ? (p0 + DF_SUB) : re;
     lds_barrier();
     [[maybe_unused]] uint64_t t0, t1, t2, t3;
     DF_T(t0);
-    uint32_t ih = p1 >= kext ? p1 - kext : 0;
+    // bytes in the ring: the sub-chunk and the next one's head
+    const uint32_t dend = DF_HEAD ? (p1 + DF_HEAD < rend ? p1 + DF_HEAD : rend) : p1;
+    uint32_t ih = dend >= kext ? dend - kext : 0;
+    if (ih > p1) ih = p1;
     if (rend >= kext && ih > rend - kext) ih = rend - kext;
     const bool link = ih > inserted;
     if (t == 0) {
@@ -853,6 +890,17 @@ __global__ __launch_bounds__(DF_THREADS) void match_kernel(DeflateParams P) {
     const bool fast = g_aligned && n0 + DF_SUB <= re;
     uint32_t nv = 0;
     if (fast) nv = reinterpret_cast<const uint32_t *>(g + n0)[t];
+    // and the head of the one after it (written with nv, after the search)
+    const uint32_t hd0 = n0 + DF_SUB;
+    const bool hload = DF_HEAD && t < (uint32_t)DF_HEAD && hd0 + t < rend;
+    uint8_t hb = 0;
+    if (hload) hb = g[hd0 + t];
+    // matches end at the block's end (or the data's)
+    uint32_t pml = p1;
+    if (DF_HEAD && p0 >= rs) {
+      const uint32_t bend = rs + ((p0 - rs) / DF_BLOCK + 1) * DF_BLOCK;
+      pml = bend < dend ? bend : dend;
+    }
     if (link) hash_keys(&s, inserted, ih, key);
     lds_barrier();
     DF_T(t1);
@@ -895,7 +943,7 @@ __global__ __launch_bounds__(DF_THREADS) void match_kernel(DeflateParams P) {
 #ifdef ZT_DF_TIME
         DF_T(w1);
 #endif
-        search_quad(&s, P, p0 + 256 * ss + 4 * (t & 63), p0, p1, key, res_out);
+        search_quad(&s, P, p0 + 256 * ss + 4 * (t & 63), p0, p1, pml, ih, key, res_out);
 #ifdef ZT_DF_TIME
         DF_T(w2);
         t_wait += w1 - w0;
@@ -926,6 +974,11 @@ __global__ __launch_bounds__(DF_THREADS) void match_kernel(DeflateParams P) {
       if (k0 == 0 && t < 16) s.ring[DF_RING / 4 + t] = nv;
     } else if (n0 < re) {
       load_sub(&s, g + n0, n0, (re - n0) < DF_SUB ? (re - n0) : DF_SUB);
+    }
+    if (hload) {
+      uint8_t *rb = reinterpret_cast<uint8_t *>(s.ring);
+      rb[ridx(hd0 + t)] = hb;
+      if (ridx(hd0 + t) < 64) rb[DF_RING + ridx(hd0 + t)] = hb;
     }
   }
 }
@@ -1648,6 +1701,8 @@ __global__ __launch_bounds__(64) void block_kernel(DeflateParams P) {
   BlockPlan *plan = P.plans + blk;
   const bool last = P.span ? lo + gspan >= n : P.final_ && (blk + nsub == P.nblocks);
   if (P.store && P.store[blk]) {  // classify_kernel: bytes that cannot beat a stored block
+    if (lane == 0) P.slot_len[blk] = blen + 5 * ((blen + 65534) / 65535) + 5;
+    if (lane > 0 && (uint32_t)lane < nsub) P.slot_len[blk + lane] = 0;
     if (lane == 0) {
       plan->ntok = 0;
       plan->btype = 0;
@@ -1839,6 +1894,9 @@ __global__ __launch_bounds__(64) void block_kernel(DeflateParams P) {
   if (P.ctype == 1) bt = 1;
   else if (stored_bits <= dyn_bits && stored_bits <= fix_bits) bt = 0;
   else bt = dyn_bits <= fix_bits ? 2 : 1;
+  // the block's exact size: scan_sizes places it before it is encoded
+  if (lane == 0) P.slot_len[blk] = (uint32_t)((bt == 0 ? stored_bits : bt == 1 ? fix_bits : dyn_bits) >> 3);
+  if (lane > 0 && (uint32_t)lane < nsub) P.slot_len[blk + lane] = 0;
   // codes for the encoder
   for (int i = lane; i < 288; i += 64) plan->lit_code[i] = bt == 2 ? (i < 286 ? s->lit_code[i] : 0u) : fixed_lit(i);
   if (lane < 32) plan->dist_code[lane] = bt == 2 ? (lane < 30 ? s->dist_code[lane] : 0u)
@@ -1916,18 +1974,37 @@ struct EncShared {
   uint32_t wsum[ENC_THREADS / 64];
 };
 
-// bit accumulator writing aligned 32-bit words of one block slot
+// a block's words in the stream: dst = the aligned word holding its first
+// byte; words 0 and `wlast` are shared with the neighbouring blocks (or the
+// restart marker), so only the block's own bytes [lo, hi) of them are stored
+struct BlockWords {
+  uint8_t *dst;
+  uint32_t wlast, lo, hi;
+  __device__ __forceinline__ void store(uint32_t w, uint32_t v) const {
+    if (w != 0 && w != wlast) {
+      reinterpret_cast<uint32_t *>(dst)[w] = v;
+      return;
+    }
+#pragma unroll
+    for (uint32_t b = 0; b < 4; ++b) {
+      const uint32_t x = 4 * w + b;
+      if (x >= lo && x < hi) dst[x] = (uint8_t)(v >> (8 * b));
+    }
+  }
+};
+
+// bit accumulator writing aligned 32-bit words of one block
 struct BitOut {
   uint64_t acc;
-  uint32_t nacc;      // valid bits in acc (acc bit 0 = bit `word * 32` of the block)
+  uint32_t nacc;      // valid bits in acc (acc bit 0 = bit `word * 32` of the block's words)
   uint32_t word;      // index of the word acc starts at
   uint32_t first;     // first word index of this thread's range
-  uint32_t *slot;
+  BlockWords slot;
   uint32_t first_val;
   bool first_partial;
   bool wrote_first;
 
-  __device__ void init(uint32_t start_bit, uint32_t *sl) {
+  __device__ void init(uint32_t start_bit, const BlockWords &sl) {
     slot = sl;
     word = start_bit >> 5;
     first = word;
@@ -1946,7 +2023,7 @@ struct BitOut {
         first_val = w;
         wrote_first = true;
       } else {
-        slot[word] = w;
+        slot.store(word, w);
       }
       ++word;
       acc >>= 32;
@@ -2020,9 +2097,32 @@ __device__ __forceinline__ void for_group_tokens(const DeflateParams &P, const B
   }
 }
 
+// bytes [src, src + n) to [dst, dst + n) by the workgroup: dst-aligned words,
+// each from two aligned source words (src may be unaligned)
+__device__ __forceinline__ void enc_copy(uint8_t *dst, const uint8_t *src, uint32_t n, uint32_t t) {
+  const uint32_t h0 = (4u - (uint32_t)((uintptr_t)dst & 3)) & 3, h = h0 < n ? h0 : n;
+  if (t < h) dst[t] = src[t];
+  const uint32_t n4 = (n - h) / 4;
+  const uint8_t *s8 = src + h;
+  uint32_t *d4 = reinterpret_cast<uint32_t *>(dst + h);
+  const uint32_t sh = (uint32_t)((uintptr_t)s8 & 3);
+  const uint32_t *s4 = reinterpret_cast<const uint32_t *>(s8 - sh);
+  const uint32_t nsrc = (sh + 4 * n4 + 3) / 4;  // source words holding bytes of the copy
+  for (uint32_t w = t; w < n4; w += ENC_THREADS) {
+    const uint32_t lo = s4[w], hi = sh && w + 1 < nsrc ? s4[w + 1] : 0u;
+    d4[w] = sh ? __builtin_amdgcn_alignbyte(hi, lo, sh) : lo;
+  }
+  for (uint32_t i = h + 4 * n4 + t; i < n; i += ENC_THREADS) dst[i] = src[i];
+}
+
+__device__ __forceinline__ bool restart_after(uint32_t b, uint32_t n, uint32_t restart, int final_,
+                                              const uint64_t *span);
+constexpr uint32_t kRestartMarkerLen = 10;
+
 // one workgroup per DEFLATE block (launched per parse block; followers
-// return): the group's stream goes to the leader's slot and on into the
-// followers' (contiguous, DF_SLOT each), whose lengths are 0
+// return): the block goes straight to its place in the stream, out +
+// boff[blk] (its size was planned exactly by block_kernel and placed by
+// scan_sizes), followed by the restart marker where a segment ends
 __global__ __launch_bounds__(ENC_THREADS) void encode_kernel(DeflateParams P) {
   __shared__ EncShared sh;
   EncShared *s = &sh;
@@ -2032,8 +2132,11 @@ __global__ __launch_bounds__(ENC_THREADS) void encode_kernel(DeflateParams P) {
   const BlockPlan *plan = P.plans + blk;
   const uint32_t bt = plan->btype, blen = plan->blen;
   const bool last = plan->last != 0;
-  uint8_t *slot_bytes = P.slots + (size_t)blk * DF_SLOT;
-  if (t > 0 && t < plan->nsub) P.slot_len[blk + t] = 0;
+  const uint8_t *slot_bytes = P.slots + (size_t)blk * DF_SLOT;
+  uint8_t *dst = P.out + P.boff[blk];
+  const uint32_t plan_bytes = P.slot_len[blk];
+  if (t < kRestartMarkerLen && restart_after(blk + plan->nsub - 1, P.nblocks, P.restart, P.final_, P.span))
+    dst[plan_bytes + t] = (t % 5) < 3 ? 0 : 0xFF;  // 00 00 00 FF FF x 2
   if (bt == 0) {
     // stored block: header byte, LEN, NLEN, data
     const uint8_t *raw = P.base + P.halo + (uint64_t)blk * DF_BLOCK;
@@ -2043,7 +2146,7 @@ __global__ __launch_bounds__(ENC_THREADS) void encode_kernel(DeflateParams P) {
     const uint32_t nparts = blen ? (blen + 65534) / 65535 : 1;
     if (t < nparts) {
       const uint32_t plen = blen - t * 65535 < 65535 ? blen - t * 65535 : 65535;
-      uint8_t *h = slot_bytes + (size_t)t * (65535 + 5);
+      uint8_t *h = dst + (size_t)t * (65535 + 5);
       h[0] = 0;
       h[1] = plen & 0xFF;
       h[2] = plen >> 8;
@@ -2051,29 +2154,17 @@ __global__ __launch_bounds__(ENC_THREADS) void encode_kernel(DeflateParams P) {
       h[4] = ((~plen) >> 8) & 0xFF;
     }
     if (t == 0) {
-      uint8_t *e = slot_bytes + 5 * nparts + blen;
+      uint8_t *e = dst + 5 * nparts + blen;
       e[0] = last ? 1 : 0;
       e[1] = 0;
       e[2] = 0;
       e[3] = 0xFF;
       e[4] = 0xFF;
-      P.slot_len[blk] = blen + 5 * nparts + 5;
+      if (blen + 5 * nparts + 5 != plan_bytes) atomicOr(P.fault, 1u);
     }
-    if (nparts == 1 && (reinterpret_cast<uintptr_t>(raw) & 3) == 0) {
-      // one piece: the data starts at slot byte 5, so slot word w (w >= 2)
-      // is raw bytes 4 w - 5 .. 4 w - 2 = one byte align of raw words w - 2,
-      // w - 1; words with header or marker bytes are written by the byte
-      // stores above and below
-      const uint32_t *raw32 = reinterpret_cast<const uint32_t *>(raw);
-      uint32_t *slot32 = reinterpret_cast<uint32_t *>(slot_bytes);
-      const uint32_t w_end = (blen + 5) / 4;  // words below hold data (and header) bytes only
-      for (uint32_t w = 2 + t; w < w_end; w += ENC_THREADS)
-        slot32[w] = __builtin_amdgcn_alignbyte(raw32[w - 1], raw32[w - 2], 3);
-      __syncthreads();  // (the word-wise stores land before the bytes around them)
-      if (t < 3 && t < blen) slot_bytes[5 + t] = raw[t];
-      for (uint32_t i = 4 * w_end - 5 + t; i < blen; i += ENC_THREADS) slot_bytes[5 + i] = raw[i];
-    } else {
-      for (uint32_t i = t; i < blen; i += ENC_THREADS) slot_bytes[5 * (i / 65535 + 1) + i] = raw[i];
+    for (uint32_t k = 0; k < nparts; ++k) {
+      const uint32_t plen = blen - k * 65535 < 65535 ? blen - k * 65535 : 65535;
+      enc_copy(dst + (size_t)k * (65535 + 5) + 5, raw + (size_t)k * 65535, plen, t);
     }
     return;
   }
@@ -2109,20 +2200,29 @@ __global__ __launch_bounds__(ENC_THREADS) void encode_kernel(DeflateParams P) {
     if (t == ENC_THREADS - 1) s->start[ENC_THREADS] = incl;
   }
   __syncthreads();
-  uint32_t *slot = reinterpret_cast<uint32_t *>(slot_bytes);
-  // thread 0 starts after the header: its complete words are in the slot
-  // already, the partial last word seeds the accumulator
-  const uint32_t start = t == 0 ? hdr_bits : s->start[t];
+  // bit positions from here on count from the aligned word holding the
+  // block's first byte: B0 bits of it belong to the previous block
+  const uint32_t B0 = 8u * (uint32_t)((uintptr_t)dst & 3);
   const uint32_t total_end = s->start[ENC_THREADS];
   // marker: 3-bit stored header (BFINAL on the stream's last block), pad, 00 00 FF FF
   const uint32_t after = total_end + 3;
   const uint32_t padded = (after + 7) & ~7u;
   const uint32_t block_end = padded + 32;
+  if (t == 0 && (block_end >> 3) != plan_bytes) atomicOr(P.fault, 1u);
+  BlockWords bw;
+  bw.dst = dst - (B0 >> 3);
+  bw.lo = B0 >> 3;
+  bw.hi = (B0 + block_end) >> 3;
+  bw.wlast = (B0 + block_end - 1) >> 5;
   BitOut bo;
-  bo.init(start, slot);
+  // thread 0 starts at the header: its complete words come from the slot
+  // (block_kernel), then its partial last word
+  bo.init(B0 + (t == 0 ? 0u : s->start[t]), bw);
   if (t == 0) {
-    bo.acc = plan->hdr_tail;
-    bo.first_partial = false;  // nothing left of thread 0 shares its first word
+    bo.first_partial = false;  // word 0's other bytes are the previous block's: stored masked (BlockWords)
+    const uint32_t *hw = reinterpret_cast<const uint32_t *>(slot_bytes);
+    for (uint32_t k = 0; k < (hdr_bits >> 5); ++k) bo.put(hw[k], 32);
+    if (hdr_bits & 31) bo.put(plan->hdr_tail, hdr_bits & 31);
   }
   if constexpr (DF_GROUP == 1)
     for_tokens(tok, a, b, [&](uint32_t tk) { put_token(bo, s, tk); });
@@ -2144,15 +2244,14 @@ __global__ __launch_bounds__(ENC_THREADS) void encode_kernel(DeflateParams P) {
     const uint32_t w = bo.word;
     uint32_t v = (uint32_t)bo.acc;
     for (uint32_t u = t + 1; u < ENC_THREADS; ++u) {
-      const uint32_t us = s->start[u], ue = (u == ENC_THREADS - 1) ? block_end : s->start[u + 1];
+      const uint32_t us = B0 + s->start[u], ue = B0 + ((u == ENC_THREADS - 1) ? block_end : s->start[u + 1]);
       if (ue == us) continue;
       if ((us >> 5) != w) break;
       v |= s->first_val[u];
       if (ue >= (w + 1) * 32) break;
     }
-    slot[w] = v;
+    bw.store(w, v);
   }
-  if (t == 0) P.slot_len[blk] = block_end >> 3;
 }
 
 // ================================ 4. stitching ================================
@@ -2163,7 +2262,6 @@ __global__ __launch_bounds__(ENC_THREADS) void encode_kernel(DeflateParams P) {
 // stored-block end marks a segment that inflate may decode on its own.
 // (a non-final call -- a shard -- also ends with the marker: the next shard
 // is independent when deflated with halo 0, see zt_shard.py)
-constexpr uint32_t kRestartMarkerLen = 10;
 __device__ __forceinline__ bool restart_after(uint32_t b, uint32_t n, uint32_t restart, int final_,
                                               const uint64_t *span) {
   if (span) {  // batch: inside a stream only (its last block carries BFINAL)
@@ -2196,35 +2294,6 @@ __global__ __launch_bounds__(1024) void scan_sizes(const uint32_t *__restrict__ 
     run += len[i] + (restart_after(i, n, restart, final_, span) ? kRestartMarkerLen : 0);
   }
   if (t == 1023) off[n] = base + part[1023];
-}
-
-__global__ __launch_bounds__(256) void gather_blocks(const uint8_t *__restrict__ slots, const uint32_t *__restrict__ len,
-                                                     const uint64_t *__restrict__ off, uint8_t *__restrict__ out,
-                                                     uint32_t nblocks, uint32_t restart, int final_,
-                                                     const uint64_t *__restrict__ span) {
-  const uint32_t b = blockIdx.x;
-  const uint8_t *src = slots + (size_t)b * DF_SLOT;
-  uint8_t *dst = out + off[b];
-  const uint32_t n = len[b];
-  if (restart_after(b, nblocks, restart, final_, span) && threadIdx.x < kRestartMarkerLen) {
-    const uint32_t i = threadIdx.x % 5;
-    dst[n + threadIdx.x] = i < 3 ? 0 : 0xFF;
-  }
-  // destination-aligned 4-byte words built from the (aligned) source with a byte shift
-  const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 3);
-  const uint32_t head = mis ? 4 - mis : 0;
-  for (uint32_t i = threadIdx.x; i < head && i < n; i += 256) dst[i] = src[i];
-  if (n > head) {
-    const uint32_t nw = (n - head) >> 2;
-    uint32_t *dw = reinterpret_cast<uint32_t *>(dst + head);
-    const uint32_t *sw = reinterpret_cast<const uint32_t *>(src);
-    const uint32_t sh = head;  // source byte offset of dst word 0 (0..3)
-    for (uint32_t i = threadIdx.x; i < nw; i += 256) {
-      uint32_t lo = sw[i], hi = sw[i + 1];
-      dw[i] = sh ? __builtin_amdgcn_alignbyte(hi, lo, sh) : lo;
-    }
-    for (uint32_t i = head + nw * 4 + threadIdx.x; i < n; i += 256) dst[i] = src[i];
-  }
 }
 
 __global__ void write_bytes(uint8_t *dst, uint64_t v, uint32_t n) {
@@ -2276,7 +2345,10 @@ static DeflateLevel level_params(int level) {
     case 7: return {64, 258, 1, 4096, 258, 8, 16, 16, 1};
     case 8: return {128, 258, 1, 4096, 258, 8, 16, 32, 1};
     case 9: return {512, 258, 1, 4096, 258, 8, 16, 258, 1};
-    default: return {32, 128, 1, 4096, 128, 8, 16, 16, 1};  // 6
+    // 6: chain 28 since matches run past 4 KiB sub-chunk ends (DF_HEAD): the
+    // 16-window gate's wordsalad worst 1.0179 (chain 32 without heads:
+    // 1.0171), 5 % less chain walking (profiles/r04j_gate.log)
+    default: return {28, 128, 1, 4096, 128, 8, 16, 16, 1};  // 6
   }
 }
 
@@ -2393,7 +2465,8 @@ int deflate_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t halo, in
   ZT_TRY(timing_begin(c, s, 1));
   P.nstore = reinterpret_cast<uint32_t *>(sb + G.res_bytes + G.slot_bytes + G.len_bytes + G.off_bytes +
                                          G.plan_bytes + ((G.nblocks + 255) & ~255u));
-  ZT_HIP(hipMemsetAsync(P.nstore, 0, 4, s));
+  P.fault = P.nstore + 1;
+  ZT_HIP(hipMemsetAsync(P.nstore, 0, 8, s));
   if (P.store) {
     classify_kernel<<<G.nblocks, 256, 0, s>>>(P);
     ZT_HIP(hipGetLastError());
@@ -2412,18 +2485,19 @@ int deflate_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t halo, in
   ZT_HIP(hipGetLastError());
   block_kernel<<<G.nblocks, 64, 0, s>>>(P);
   ZT_HIP(hipGetLastError());
-  encode_kernel<<<G.nblocks, ENC_THREADS, 0, s>>>(P);
-  ZT_HIP(hipGetLastError());
   scan_sizes<<<1, 1024, 0, s>>>(P.slot_len, G.nblocks, off, 0, P.restart, final_, nullptr);
   ZT_HIP(hipGetLastError());
-  gather_blocks<<<G.nblocks, 256, 0, s>>>(P.slots, P.slot_len, off, d_out, G.nblocks, P.restart, final_, nullptr);
+  P.out = d_out;
+  P.boff = off;
+  encode_kernel<<<G.nblocks, ENC_THREADS, 0, s>>>(P);
   ZT_HIP(hipGetLastError());
   ZT_TRY(timing_end(c, s, 1));
   uint64_t total = 0;
-  uint32_t nst[1] = {0};  // blocks stored unsearched
+  uint32_t nst[2] = {0, 0};  // blocks stored unsearched, encode faults
   ZT_HIP(hipMemcpyAsync(&total, off + G.nblocks, sizeof total, hipMemcpyDeviceToHost, s));
-  ZT_HIP(hipMemcpyAsync(nst, P.nstore, 4, hipMemcpyDeviceToHost, s));
+  ZT_HIP(hipMemcpyAsync(nst, P.nstore, 8, hipMemcpyDeviceToHost, s));
   ZT_HIP(hipStreamSynchronize(s));
+  if (nst[1]) return set_error(ZT_E_INTERNAL, "deflate: a block's encoded size differs from its plan");
   c->times.blocks_unsearched += nst[0];
   ZT_TRY(timing_collect(c, &c->times.deflate_ms, &c->times.deflate_launches, 0));
   ZT_TRY(timing_collect(c, &c->times.deflate_pipeline_ms, &c->times.deflate_pipelines, 1));
@@ -2498,7 +2572,8 @@ int deflate_batch_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t count, const
   ZT_TRY(timing_begin(c, s, 1));
   P.nstore = reinterpret_cast<uint32_t *>(sb + G.res_bytes + G.slot_bytes + G.len_bytes + G.off_bytes +
                                          G.plan_bytes + ((G.nblocks + 255) & ~255u));
-  ZT_HIP(hipMemsetAsync(P.nstore, 0, 4, s));
+  P.fault = P.nstore + 1;
+  ZT_HIP(hipMemsetAsync(P.nstore, 0, 8, s));
   if (P.store) {
     classify_kernel<<<G.nblocks, 256, 0, s>>>(P);
     ZT_HIP(hipGetLastError());
@@ -2517,18 +2592,19 @@ int deflate_batch_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t count, const
   ZT_HIP(hipGetLastError());
   block_kernel<<<G.nblocks, 64, 0, s>>>(P);
   ZT_HIP(hipGetLastError());
-  encode_kernel<<<G.nblocks, ENC_THREADS, 0, s>>>(P);
-  ZT_HIP(hipGetLastError());
   scan_sizes<<<1, 1024, 0, s>>>(P.slot_len, G.nblocks, d_off, 0, P.restart, 1, d_span);
   ZT_HIP(hipGetLastError());
-  gather_blocks<<<G.nblocks, 256, 0, s>>>(P.slots, P.slot_len, d_off, d_out, G.nblocks, P.restart, 1, d_span);
+  P.out = d_out;
+  P.boff = d_off;
+  encode_kernel<<<G.nblocks, ENC_THREADS, 0, s>>>(P);
   ZT_HIP(hipGetLastError());
   ZT_TRY(timing_end(c, s, 1));
   std::vector<uint64_t> boff((size_t)G.nblocks + 1);
-  uint32_t nst[1] = {0};  // blocks stored unsearched
+  uint32_t nst[2] = {0, 0};  // blocks stored unsearched, encode faults
   ZT_HIP(hipMemcpyAsync(boff.data(), d_off, boff.size() * 8, hipMemcpyDeviceToHost, s));
-  ZT_HIP(hipMemcpyAsync(nst, P.nstore, 4, hipMemcpyDeviceToHost, s));
+  ZT_HIP(hipMemcpyAsync(nst, P.nstore, 8, hipMemcpyDeviceToHost, s));
   ZT_HIP(hipStreamSynchronize(s));
+  if (nst[1]) return set_error(ZT_E_INTERNAL, "deflate: a block's encoded size differs from its plan");
   c->times.blocks_unsearched += nst[0];
   ZT_TRY(timing_collect(c, &c->times.deflate_ms, &c->times.deflate_launches, 0));
   ZT_TRY(timing_collect(c, &c->times.deflate_pipeline_ms, &c->times.deflate_pipelines, 1));

@@ -127,7 +127,10 @@ static int batch_two_phase(DeviceCtx *c, const uint8_t *d_in, const std::vector<
       continue;
     }
     desc_total = align_up(desc_total, 512);
-    segs.push_back(SegJob{(uint32_t)chain.size(), 1});
+    // (a stream of stored runs only: expand_kernel writes it straight from
+    // the input, copy_kernel skips its segment -- inflate_seg.hip)
+    const bool direct = (r.ntok >> 30) == 3u;
+    segs.push_back(SegJob{(uint32_t)chain.size(), direct ? 0x80000001u : 1u});
     chain.push_back(ChainUnit{jobs[k].tok_off, out_total, out_total, desc_total, r.ntok, (uint32_t)r.out_len});
     who.push_back(k);
     out_total += align_up(r.out_len ? r.out_len : 1, 256);

@@ -439,6 +439,18 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
     if (nx <= u || nx >= units) FALLBACK("unit %zu: bad stop %d\n", u, r.stop_idx);
     u = nx;
   }
+  // a segment of units that hold stored runs only (TokResult ntok bit 30;
+  // or nothing) is written by expand_kernel straight from the input and
+  // skipped by copy_kernel (SegJob count bit 31); elsewhere bit 30 is cleared
+  for (SegJob &sj : segs) {
+    bool direct = true;
+    for (uint32_t k = 0; k < sj.count; ++k) {
+      const ChainUnit &cu = chain[sj.first + k];
+      direct = direct && ((cu.ntok >> 30) == 3u || cu.out_len == 0);  // (empty units: the restart markers)
+    }
+    for (uint32_t k = 0; k < sj.count && !direct; ++k) chain[sj.first + k].ntok &= ~0x40000000u;
+    if (direct) sj.count |= 0x80000000u;
+  }
   *out_len = total;
   *end_ip = (res[u].end_bits + 7) >> 3;
   if (inf_debug()) {
@@ -446,7 +458,7 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
     uint64_t mn = ~0ull, mx = 0;
     size_t small = 0;
     for (size_t i = 0; i < segs.size(); ++i) {
-      const ChainUnit &a = chain[segs[i].first], &b = chain[segs[i].first + segs[i].count - 1];
+      const ChainUnit &a = chain[segs[i].first], &b = chain[segs[i].first + (segs[i].count & 0x7FFFFFFFu) - 1];
       const uint64_t len = b.out_off + b.out_len - a.out_off;
       mn = len < mn ? len : mn;
       mx = len > mx ? len : mx;

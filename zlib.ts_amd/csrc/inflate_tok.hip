@@ -65,6 +65,7 @@ __global__ __launch_bounds__(64) ZT_TOK_ATTR void tokenize_kernel(TokParams P) {
   uint64_t si = job.stop_first;
   bool bfinal = false;
   bool any_run = false;  // run tokens written (flag bit 31 of the result's ntok: expand_kernel's run path)
+  bool other = false;    // tokens that are not runs (bit 30 of ntok: every output byte comes from a run)
   g_u8 *gin = (g_u8 *)P.in;
   while (!bfinal) {
     uint32_t v;
@@ -101,6 +102,7 @@ __global__ __launch_bounds__(64) ZT_TOK_ATTR void tokenize_kernel(TokParams P) {
           to.emit((uint32_t)(p >> 32));
           any_run = true;
         } else {
+          other = true;
           to.flush_partial();
           for (uint32_t j = lane; j < len; j += 64) to.tok[nt0 + j] = gin[p + j];
           const uint32_t nt = nt0 + len;
@@ -112,6 +114,7 @@ __global__ __launch_bounds__(64) ZT_TOK_ATTR void tokenize_kernel(TokParams P) {
       }
       rd.seek_byte(p + len);
     } else {
+      other = true;
       status = read_tables<false>(rd, sh.lens, &sh.lit, &sh.dist, btype, lane, detail);
       if (status) break;
       uint64_t end_bit = 0;
@@ -174,7 +177,7 @@ __global__ __launch_bounds__(64) ZT_TOK_ATTR void tokenize_kernel(TokParams P) {
     TokResult r;
     r.out_len = op;
     r.end_bits = rd.pos_bits_in();
-    r.ntok = to.ntok | (any_run ? 0x80000000u : 0u);
+    r.ntok = to.ntok | (any_run ? 0x80000000u : 0u) | (any_run && !other ? 0x40000000u : 0u);
     r.status = status;
     r.detail = detail;
     r.stop_idx = stop_idx;
@@ -235,7 +238,7 @@ __device__ __forceinline__ void expand_unit(const ResolveParams &P, ExpandShared
   const uint32_t u = blockIdx.x;
   const int lane = threadIdx.x & 63;
   const uint32_t *tk = P.tokens + cu.tok_off;
-  const uint32_t ntok = cu.ntok & 0x7FFFFFFFu;
+  const uint32_t ntok = cu.ntok & 0x3FFFFFFFu;
   const uint32_t nchunks = (ntok + 63) / 64;
   uint16_t *desc = P.desc + cu.desc_off;
   const uint64_t back = cu.out_off - cu.seg_off;  // bytes of the segment before this unit
@@ -382,10 +385,70 @@ __device__ __forceinline__ void expand_unit(const ResolveParams &P, ExpandShared
   if (lane == 0) P.unit_status[u] = any_bad ? ZT_E_INVALID_DISTANCE : (op != cu.out_len ? ZT_E_INPUT_BROKEN : ZT_OK);
 }
 
+// bytes [src, src + n) to [dst, dst + n) by one wave: dst-aligned words
+// (each from two aligned source words), 4 per lane in flight
+__device__ __forceinline__ void wave_copy(uint8_t *dst, const uint8_t *src, uint32_t n, int lane) {
+  const uint32_t h = ((4u - (uint32_t)((uintptr_t)dst & 3)) & 3) < n ? ((4u - (uint32_t)((uintptr_t)dst & 3)) & 3) : n;
+  if ((uint32_t)lane < h) dst[lane] = src[lane];
+  const uint32_t n4 = (n - h) / 4;
+  const uint8_t *s = src + h;
+  uint32_t *d4 = reinterpret_cast<uint32_t *>(dst + h);
+  const uint32_t sh = (uint32_t)((uintptr_t)s & 3);
+  const uint32_t *s4 = reinterpret_cast<const uint32_t *>(s - sh);
+  // source words [0, nw) exist: the last one a full word only when the copy
+  // reaches it (no read past the payload's last byte)
+  const uint32_t nsrc = (sh + 4 * n4 + 3) / 4;
+  for (uint32_t w0 = 0; w0 < n4; w0 += 256) {
+    uint32_t v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t w = w0 + 64 * k + (uint32_t)lane;
+      uint32_t lo = 0, hi = 0;
+      if (w < n4) {
+        lo = s4[w];
+        hi = sh && w + 1 < nsrc ? s4[w + 1] : 0u;
+      }
+      v[k] = sh ? __builtin_amdgcn_alignbyte(hi, lo, sh) : lo;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t w = w0 + 64 * k + (uint32_t)lane;
+      if (w < n4) d4[w] = v[k];
+    }
+  }
+  for (uint32_t i = h + 4 * n4 + (uint32_t)lane; i < n; i += 64) dst[i] = src[i];
+}
+
+// a unit whose every output byte is a stored run, in a segment of such units
+// (ChainUnit ntok bit 30, set by the host): the runs go from the input
+// straight to their final place (copy_kernel skips the segment) -- 1 byte
+// read and 1 written per byte instead of descriptors written and read back
+__device__ __forceinline__ void expand_direct(const ResolveParams &P, const ChainUnit &cu) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t *tk = P.tokens + cu.tok_off;
+  const uint32_t ntok = cu.ntok & 0x3FFFFFFFu;
+  uint32_t op = 0;
+  bool ok = ntok % 3 == 0;
+  for (uint32_t i = 0; ok && i < ntok; i += 3) {
+    const uint32_t t0 = tk[i], lo = tk[i + 1], hi = tk[i + 2];
+    const uint32_t rl = t0 >> 16;
+    if ((t0 & 0xFFFFu) || rl == 0 || op + rl > cu.out_len) {
+      ok = false;
+      break;
+    }
+    const uint64_t src = (uint64_t)lo | ((uint64_t)hi << 32);
+    wave_copy(P.out + cu.out_off + op, P.in + src, rl, lane);
+    op += rl;
+  }
+  if (lane == 0) P.unit_status[blockIdx.x] = ok && op == cu.out_len ? ZT_OK : ZT_E_INPUT_BROKEN;
+}
+
 __global__ __launch_bounds__(64) void expand_kernel(ResolveParams P) {
   __shared__ ExpandShared sh;
   const ChainUnit cu = P.units[blockIdx.x];
-  if (cu.ntok >> 31)
+  if ((cu.ntok >> 30) == 3u)
+    expand_direct(P, cu);
+  else if (cu.ntok >> 31)
     expand_unit<true>(P, sh, cu);
   else
     expand_unit<false>(P, sh, cu);
@@ -443,7 +506,11 @@ __global__ __launch_bounds__(64) void copy_kernel(ResolveParams P) {
 #endif
   const uint32_t sg = blockIdx.x;
   const int lane = threadIdx.x & 63;
-  const SegJob sj = P.segs[sg];
+  SegJob sj = P.segs[sg];
+  if (sj.count >> 31) {  // stored runs only: expand_kernel wrote the bytes
+    if (lane == 0) P.seg_status[sg] = ZT_OK;
+    return;
+  }
   const uint64_t seg_out = P.units[sj.first].out_off;
   const ChainUnit lastu = P.units[sj.first + sj.count - 1];
   const uint64_t n = lastu.out_off + lastu.out_len - seg_out;  // segment bytes
