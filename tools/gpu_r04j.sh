@@ -14,3 +14,6 @@ timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-ap
 tail -1 gpurun_out/r04j/bench.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print("bench", d["value"], d["ratio"], d["deflate_pipeline_ms"], d["match_kernel_ms"], d["inflate_kernel_ms"], d.get("ratio_vs_ref"))'
 ZT_INF_TIMING=1 timeout -k 10 120 python tools/inf_timing.py > gpurun_out/r04j/inf_timing.log 2>&1
 tail -14 gpurun_out/r04j/inf_timing.log
+export TMPDIR=/tmp
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $R/gpurun_out/r04j/prof -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-api > $R/gpurun_out/r04j/prof.log 2>&1
+cd $R && cut -d, -f1-4 gpurun_out/r04j/prof/run_kernel_stats.csv | head -16 | sed 's/(zt::[A-Za-z]*)//; s/"zt::(anonymous namespace):://'

@@ -594,7 +594,7 @@ __device__ __forceinline__ uint32_t near_any(const uint32_t (&w)[9], uint32_t cu
 struct Walk {
   uint32_t p, q, link, max_len, best_len, best_dist, o, pw, omask, cur, cur2, cur3, cur4;
   uint32_t cl;  // carried match length (kept unless the walk finds one at least as long, nearer)
-  int hops, max_hops;
+  int max_hops;  // (hops taken = the pair loop's step count while the walk is active)
   bool active;
 };
 
@@ -628,7 +628,6 @@ __device__ __forceinline__ void walk_init(Walk &w, const MatchShared *s, const D
     w.best_len = carry_len - 1 < w.max_len ? carry_len - 1 : w.max_len;
     w.best_dist = carry_dist;
   }
-  w.hops = 0;
   w.max_hops = (int)w.best_len >= P.good ? (P.max_chain >> 2) : P.max_chain;
   w.active = w.max_len >= (uint32_t)P.klen && (int)w.best_len < P.skip_len;
   w.cl = w.best_len;
@@ -700,17 +699,20 @@ __device__ __forceinline__ void walk_extend(Walk &w, const MatchShared *s, const
 // one hop of two walks: every LDS load of both hops is issued before any is
 // used (the walks are latency-bound pointer chases), then the checks.  Per
 // hop two loads: the link and the filter word.
-__device__ __forceinline__ void walk_pair_step(Walk &a, Walk &b, const MatchShared *s, const DeflateParams &P) {
-  const uint32_t qa = a.active ? a.q - a.link : a.q;
-  const uint32_t qb = b.active ? b.q - b.link : b.q;
+// `step`: the pair loop's count of steps before this one (wave-uniform): an
+// active walk has taken exactly that many hops.  Inactive walks keep
+// stepping through stale links: their loads stay inside the ring and are
+// never used.
+__device__ __forceinline__ void walk_pair_step(Walk &a, Walk &b, const MatchShared *s, const DeflateParams &P,
+                                               int step) {
+  const uint32_t qa = a.q - a.link;
+  const uint32_t qb = b.q - b.link;
   const bool ha = a.active && a.p - qa <= (uint32_t)DF_MAXDIST;
   const bool hb = b.active && b.p - qb <= (uint32_t)DF_MAXDIST;
   const uint32_t la = s->prev[ridx(qa)], lb = s->prev[ridx(qb)];
   const uint32_t oa = ld32(s, qa + a.o), ob = ld32(s, qb + b.o);
   a.q = qa;
   b.q = qb;
-  a.hops += ha ? 1 : 0;
-  b.hops += hb ? 1 : 0;
 #ifdef ZT_DF_COUNT
   if ((threadIdx.x & 63) == 0) atomicAdd(&g_df_count[0], 1ull);
   atomicAdd(&g_df_count[1], (unsigned long long)(ha ? 1 : 0) + (hb ? 1 : 0));
@@ -719,8 +721,8 @@ __device__ __forceinline__ void walk_pair_step(Walk &a, Walk &b, const MatchShar
   const bool cb = hb && ((ob ^ b.pw) & b.omask) == 0;
   a.link = la;
   b.link = lb;
-  a.active = ha && la != 0 && a.hops < a.max_hops;
-  b.active = hb && lb != 0 && b.hops < b.max_hops;
+  a.active = ha && la != 0 && step + 1 < a.max_hops;
+  b.active = hb && lb != 0 && step + 1 < b.max_hops;
   if (ca) walk_extend(a, s, P, qa);
   if (cb) walk_extend(b, s, P, qb);
 }
@@ -783,7 +785,7 @@ __device__ void search_quad(const MatchShared *s, const DeflateParams &P, uint32
   Walk wa, wb;
   walk_init(wa, s, P, pb, pml, win32<16>(w), win32<20>(w), win32<24>(w), win32<28>(w), 0, 0);
   walk_init(wb, s, P, pb + 2, pml, win32<18>(w), win32<22>(w), win32<26>(w), win32<30>(w), 0, 0);
-  while (wa.active || wb.active) walk_pair_step(wa, wb, s, P);
+  for (int step = 0; wa.active || wb.active; ++step) walk_pair_step(wa, wb, s, P, step);
   out[0] = walk_finish<0>(wa, s, P, w, nr0, lim4, c0l, c0d);
   out[2] = walk_finish<2>(wb, s, P, w, nr2, lim4, c2l, c2d);
 #ifdef ZT_DF_NOCARRY  // experiment: positions 1 and 3 start without the carried match
@@ -791,7 +793,7 @@ __device__ void search_quad(const MatchShared *s, const DeflateParams &P, uint32
 #endif
   walk_init(wa, s, P, pb + 1, pml, win32<17>(w), win32<21>(w), win32<25>(w), win32<29>(w), c0l, c0d);
   walk_init(wb, s, P, pb + 3, pml, win32<19>(w), win32<23>(w), win32<27>(w), win32<31>(w), c2l, c2d);
-  while (wa.active || wb.active) walk_pair_step(wa, wb, s, P);
+  for (int step = 0; wa.active || wb.active; ++step) walk_pair_step(wa, wb, s, P, step);
   out[1] = walk_finish<1>(wa, s, P, w, nr1, lim4, cl, cd);
   out[3] = walk_finish<3>(wb, s, P, w, nr3, lim4, cl, cd);
   // the positions' own bytes (res_pack)
