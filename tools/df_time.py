@@ -16,6 +16,9 @@ for kind in sys.argv[1:]:
     zt.lib.zt_debug_df_time(buf)
     v = list(buf)
     ws = v[3]  # (wave, sub-chunk) pairs
+    if ws == 0:
+        print(f"{kind:10s} no sub-chunk searched (every block stored by classify_kernel)", flush=True)
+        continue
     subs = ws / 16
     print(f"{kind:10s} per wave per sub-chunk: hash {v[0]/ws:7.0f}  link(2 waves) {v[4]/subs/2:7.0f}  "
           f"link-wait {v[5]/ws:7.0f}  search {v[1]/ws:7.0f}  loop total {v[7]/ws:7.0f}  barrier idle {v[2]/ws:7.0f}  "

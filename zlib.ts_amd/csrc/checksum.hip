@@ -20,7 +20,8 @@
 //   * Adler: v_dot4_u32_u8 sums per 16-byte piece, positions weighted from
 //     the piece's place in the segment;
 //   * per-lane results are merged with polynomial shifts (CRC) and weighted
-//     sums (Adler) inside the workgroup, then one tiny kernel merges segments.
+//     sums (Adler) inside the workgroup; segments merge by atomics and the
+//     last workgroup to finish writes the result (batch: a small kernel).
 //     Ragged first / last segments take a byte-wise per-thread-slice path
 //     (slice-by-8 through nibble tables in LDS).
 // Algorithmic bytes per unit: N input bytes read.
@@ -263,6 +264,19 @@ __device__ inline uint32_t shift_bytes(const uint32_t *__restrict__ dig, const u
   return c;
 }
 
+// One buffer's merge inside checksum_segments: every workgroup adds its
+// segments' (already end-shifted) results to `acc` by atomics, workgroup 0
+// adds the caller's initial CRC shifted over the whole buffer, and the
+// workgroup that arrives last writes the final values and leaves `acc`
+// zeroed for the next call (calls on a context are serialised by its mutex).
+// A separate one-workgroup finish kernel cost 6 us + its launch per call.
+struct CkFinish {
+  CkAcc *acc;  // null: batch mode (per-segment results to `out`)
+  uint32_t *result;
+  uint64_t n;
+  uint32_t crc_in, adler_in;
+};
+
 template <bool DO_CRC, bool DO_ADLER>
 __global__ __launch_bounds__(CK_THREADS, ZT_CK_MINW) void checksum_segments(const uint8_t *__restrict__ frame0, size_t lo0,
                                                                  size_t hi0, size_t nseg,
@@ -270,7 +284,7 @@ __global__ __launch_bounds__(CK_THREADS, ZT_CK_MINW) void checksum_segments(cons
                                                                  const uint32_t *__restrict__ x2n_g,
                                                                  const uint32_t *__restrict__ shift_g,
                                                                  SegResult *__restrict__ out,
-                                                                 const CkJob *__restrict__ jobs = nullptr) {
+                                                                 const CkJob *__restrict__ jobs, CkFinish fin) {
   // 32 KiB of replicated nibble tables + the combine scratch
   __shared__ uint32_t T[DO_CRC ? 256 * 32 : 1];  // nibble positions 0..15 (ragged slices only)
   __shared__ uint32_t x2n[32];
@@ -295,6 +309,8 @@ __global__ __launch_bounds__(CK_THREADS, ZT_CK_MINW) void checksum_segments(cons
   }
   __syncthreads();
 
+  uint32_t wg_crc = 0;  // thread 0: this workgroup's merged segments (fin.acc)
+  uint64_t wg_s1 = 0, wg_s2 = 0;
   for (size_t seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
     // one buffer, or (batch) segment k of buffer `jobs[seg]` (16-byte aligned)
     const uint8_t *frame = frame0;
@@ -548,61 +564,43 @@ __global__ __launch_bounds__(CK_THREADS, ZT_CK_MINW) void checksum_segments(cons
         r.s1 = (uint32_t)(t1 % 65521u);
         r.s2 = (uint32_t)((t2 % 65521u + (after % 65521u) * r.s1) % 65521u);
         r.len = sv_hi > sv_lo ? (uint32_t)(sv_hi - sv_lo) : 0;
-        out[seg] = r;
+        if (fin.acc) {
+          wg_crc ^= r.crc;
+          wg_s1 += r.s1;
+          wg_s2 += r.s2;
+        } else {
+          out[seg] = r;
+        }
       }
     }
     __syncthreads();
   }
-}
-
-// Merge per-segment results (already moved to the end of the buffer by
-// checksum_segments) and apply the callers' initial values.
-#define CF_THREADS 1024
-__global__ __launch_bounds__(CF_THREADS) void checksum_finish(const SegResult *__restrict__ segs, size_t nseg,
-                                                              size_t hi, uint64_t n,
-                                                              const uint32_t *__restrict__ x2n_g,
-                                                              const uint32_t *__restrict__ shift_g, uint32_t crc_in,
-                                                              uint32_t adler_in, uint32_t *__restrict__ result) {
-  __shared__ uint32_t red_c[CF_THREADS / 64];
-  __shared__ uint64_t red_1[CF_THREADS / 64], red_2[CF_THREADS / 64];
-  const uint32_t *dig = shift_g + ZT_CRC_DIG_OFF;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  uint32_t c = 0;
-  uint64_t t1 = 0, t2 = 0;
-  for (size_t i = tid; i < nseg; i += CF_THREADS) {
-    const SegResult r = segs[i];
-    c ^= r.crc;
-    t1 += r.s1;
-    t2 += r.s2;
-  }
-  for (int o = 32; o; o >>= 1) {
-    c ^= __shfl_xor(c, o);
-    t1 += __shfl_xor(t1, o);
-    t2 += __shfl_xor(t2, o);
-  }
-  if (lane == 0) {
-    red_c[wv] = c;
-    red_1[wv] = t1;
-    red_2[wv] = t2;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    uint32_t raw = 0;
-    uint64_t r1 = 0, r2 = 0;
-    for (int w = 0; w < CF_THREADS / 64; ++w) {
-      raw ^= red_c[w];
-      r1 += red_1[w];
-      r2 += red_2[w];
+  if (fin.acc && tid == 0) {
+    // CRC32.update: ~(shift(~crc_in, n) ^ raw); Adler32.update below
+    if (DO_CRC && blockIdx.x == 0) wg_crc ^= shift_bytes(shift_g + ZT_CRC_DIG_OFF, x2n, fin.n, ~fin.crc_in);
+    // Device-scope atomics are performed past the XCD's L2, and a returned
+    // value means this one has been: the done count is bumped only after the
+    // three sums have landed, so no __threadfence (an L2 write-back +
+    // invalidate per workgroup, which made the kernel 0.223 -> 0.258 ms)
+    CkAcc *a = fin.acc;
+    uint32_t landed = 0;
+    if (DO_CRC) landed ^= atomicXor(&a->crc, wg_crc);
+    if (DO_ADLER) {
+      landed ^= (uint32_t)atomicAdd(&a->s1, (unsigned long long)wg_s1);
+      landed ^= (uint32_t)atomicAdd(&a->s2, (unsigned long long)wg_s2);
     }
-    r1 %= 65521u;
-    r2 %= 65521u;
-    // CRC32.update: ~(shift(~crc, n) ^ raw)
-    result[0] = ~(shift_bytes(dig, x2n_g, n, ~crc_in) ^ raw);
-    // Adler32.update: s1 = adler & 0xFFFF, s2 = (adler >> 16) & 0xFFFF (need not be reduced)
-    uint64_t a = adler_in & 0xFFFFu, bb = (adler_in >> 16) & 0xFFFFu;
-    uint64_t f1 = (a + r1) % 65521u;
-    uint64_t f2 = (bb + (n % 65521u) * (a % 65521u) + r2) % 65521u;
-    result[1] = (uint32_t)((f2 << 16) | f1);
+    asm volatile("" ::"v"(landed) : "memory");  // waits for the returns
+    if (atomicAdd(&a->done, 1u) == gridDim.x - 1) {
+      const uint32_t raw = atomicExch(&a->crc, 0u);
+      const uint64_t r1 = atomicExch(&a->s1, 0ull) % 65521u, r2 = atomicExch(&a->s2, 0ull) % 65521u;
+      atomicExch(&a->done, 0u);
+      fin.result[0] = ~raw;
+      // s1 = adler & 0xFFFF, s2 = (adler >> 16) & 0xFFFF (need not be reduced)
+      const uint64_t a1 = fin.adler_in & 0xFFFFu, a2 = (fin.adler_in >> 16) & 0xFFFFu;
+      const uint64_t f1 = (a1 + r1) % 65521u;
+      const uint64_t f2 = (a2 + (fin.n % 65521u) * (a1 % 65521u) + r2) % 65521u;
+      fin.result[1] = (uint32_t)((f2 << 16) | f1);
+    }
   }
 }
 
@@ -701,7 +699,7 @@ int checksums_batch_dev(DeviceCtx *c, const uint8_t *frame, size_t count, const 
   ZT_HIP(hipMemcpy(d_len, len, count * 8, hipMemcpyHostToDevice));
   if (nj) {
     checksum_segments<true, true><<<(unsigned)nj, CK_THREADS, 0, s>>>(frame, 0, 0, nj, c->d_crc_nib, c->d_crc_x2n,
-                                                                      c->d_crc_shift, d_seg, d_jobs);
+                                                                      c->d_crc_shift, d_seg, d_jobs, CkFinish{});
     ZT_HIP(hipGetLastError());
   }
   checksum_batch_finish<<<(unsigned)((count + 255) / 256), 256, 0, s>>>(d_seg, d_first, d_len, (uint32_t)count,
@@ -720,17 +718,16 @@ int checksums_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, bool do_crc, bool
   ZT_TRY(scratch(c, 8, nseg * sizeof(SegResult), &segbuf));
   SegResult *segs = static_cast<SegResult *>(segbuf);
   const int grid = (int)(nseg < (size_t)c->num_cu * 8 ? nseg : (size_t)c->num_cu * 8);
+  const CkFinish fin{c->d_ck_acc, d_result, n, crc_in, adler_in};
   if (do_crc && do_adler)
     checksum_segments<true, true><<<grid, CK_THREADS, 0, s>>>(frame, lo, hi, nseg, c->d_crc_nib, c->d_crc_x2n,
-                                                              c->d_crc_shift, segs);
+                                                              c->d_crc_shift, segs, nullptr, fin);
   else if (do_crc)
     checksum_segments<true, false><<<grid, CK_THREADS, 0, s>>>(frame, lo, hi, nseg, c->d_crc_nib, c->d_crc_x2n,
-                                                               c->d_crc_shift, segs);
+                                                               c->d_crc_shift, segs, nullptr, fin);
   else
     checksum_segments<false, true><<<grid, CK_THREADS, 0, s>>>(frame, lo, hi, nseg, c->d_crc_nib, c->d_crc_x2n,
-                                                               c->d_crc_shift, segs);
-  ZT_HIP(hipGetLastError());
-  checksum_finish<<<1, CF_THREADS, 0, s>>>(segs, nseg, hi, n, c->d_crc_x2n, c->d_crc_shift, crc_in, adler_in, d_result);
+                                                               c->d_crc_shift, segs, nullptr, fin);
   ZT_HIP(hipGetLastError());
   return ZT_OK;
 }

@@ -13,14 +13,17 @@ constexpr int RING = 32768;
 constexpr uint32_t RING_MASK = RING - 1;
 constexpr int GRAN = 16384;  // output flush granule (ring holds 32 KiB of history)
 #ifndef ZT_PRI
-#define ZT_PRI 7
+#define ZT_PRI 8
 #endif
 constexpr int PRI = ZT_PRI;
 
-// PRI: primary table bits.  7 (512 B per table) rather than 10: the decode
-// kernels' LDS shrinks enough for more units per CU, which outweighs the
-// canonical search of the rarer longer codes (tokenize 5.9 -> 5.1 ms per GiB;
-// measured 6..10).
+// PRI: primary table bits.  8 (1 KiB per table): every 8-bit code -- all
+// literals of the reference's blocks over random bytes -- decodes from one
+// lookup instead of the canonical search's three dependent LDS reads
+// (tokenize of the C2 batch 15.5 -> 11.5 ms, bench 4.05 -> 3.94 ms per GiB;
+// profiles/r04pri_*).  tokenize_kernel's 12.5 KiB of LDS still allows the
+// 12 units per CU its registers allow (3 waves per SIMD).  Round 1 chose 7
+// over 8..10 when LDS, not registers, set the units per CU.
 // Primary-table entry (u32): bits 0-3 code length (0 = code longer than PRI
 // bits: canonical search), 4-7 extra bits, 8-16 symbol, 17-31 base value
 // (match length for literal/length symbols > 256, distance for distance

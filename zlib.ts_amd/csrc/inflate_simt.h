@@ -319,33 +319,105 @@ __device__ __forceinline__ bool near_fixed_code(const HuffTab *lt) {
   return mx >= 29491u;
 }
 
-__device__ uint64_t lane_phase_map(LaneBits &lb, uint64_t b0, uint32_t s_l, uint32_t limit, bool in_range,
-                                   const HuffTab *lt, const HuffTab *dt) {
-  uint64_t map = ~0ull;
+#ifndef ZT_PM_N
+#define ZT_PM_N 3  // 161 VGPRs (3 waves per SIMD); C2 tokenize 5.20 / 5.23 / 5.33 ms with 3 / 4 / 5 (4: one VGPR spilled, 5: three)
+#endif
+constexpr int PM_N = ZT_PM_N;  // start phases decoded side by side per lane
+
+// one start phase's decode: >= 32 valid bits in bb at every step
+struct PhaseDec {
+  uint64_t bb;
+  uint32_t bc, q, rel, ph;
+  bool act;
+};
+
+// map[x], x = 0 .. maxlen - 1: the phase past s_next at which the decode from
+// s_l + x crosses into the next lane (15: it ends the block, breaks, or
+// crosses 15 or more bits past it).  ph0 <= 15: map[0] is known (a first
+// pass decoded from s_l); 16: decoded here too.  The
+// other phases go PM_N at a time: each step issues every decode's next input
+// word and primary-table entry before any is used (one LDS round trip per
+// step for all of them, where one decode at a time waited for each); a
+// literal from the primary table -- nearly every token of these blocks -- is
+// consumed inline, anything else takes lane_token.
+__device__ uint64_t lane_phase_map(const LaneBits &lb, uint64_t b0, uint32_t s_l, uint32_t limit, bool in_range,
+                                   uint32_t ph0, const HuffTab *lt, const HuffTab *dt) {
+  constexpr uint32_t M = (1u << PRI) - 1;
   const uint32_t s_next = s_l + SP_LANE_BITS;
   // a token boundary lies within the longest code past s_l when the token
   // straddling s_l is a literal (matches are rare in these blocks; a phase
   // not mapped stays 15 = unknown, and that lane takes the ordinary repair)
   const uint32_t xmax = lt->maxlen < 15 ? (uint32_t)lt->maxlen : 15u;
+  uint64_t map = ph0 > 15 ? ~0ull : (~0xFull | ph0);
 #pragma unroll 1
-  for (uint32_t x = 0; x < xmax; ++x) {
-    bool act = in_range;
-    if (act) lb.init(b0 + s_l + x, s_l + x);
-    uint32_t ph = 15;
-    while (__ballot(act)) {
-      if (act) {
-        uint32_t tk, nb;
-        const int r = lane_token(lb, lt, dt, tk, nb);
-        if (r != 0 || lb.rel > limit) {
-          act = false;
-        } else if (lb.rel >= s_next) {
-          const uint32_t d = lb.rel - s_next;
-          ph = d < 15 ? d : 15;
-          act = false;
+  for (uint32_t x0 = ph0 > 15 ? 0u : 1u; x0 < xmax; x0 += PM_N) {
+    PhaseDec d[PM_N];
+#pragma unroll
+    for (int k = 0; k < PM_N; ++k) {
+      const uint64_t abs_bit = b0 + s_l + x0 + k;
+      const uint32_t q = (uint32_t)(abs_bit >> 5), sh = (uint32_t)abs_bit & 31;
+      d[k].bb = (((uint64_t)lb.word(q + 1) << 32) | lb.word(q)) >> sh;
+      d[k].bc = 64 - sh;
+      d[k].q = q + 2;
+      d[k].rel = s_l + x0 + k;
+      d[k].ph = 15;
+      d[k].act = in_range && x0 + k < xmax;
+    }
+    for (;;) {
+      bool any = false;
+#pragma unroll
+      for (int k = 0; k < PM_N; ++k) any = any || d[k].act;
+      if (!__ballot(any)) break;
+      uint32_t w[PM_N], e[PM_N];
+#pragma unroll
+      for (int k = 0; k < PM_N; ++k) {
+        w[k] = lb.word(d[k].q);
+        e[k] = lt->pri[(uint32_t)d[k].bb & M];
+      }
+#pragma unroll
+      for (int k = 0; k < PM_N; ++k) {
+        PhaseDec &r = d[k];
+        if (!r.act) continue;
+        if ((e[k] & 15) && ((e[k] >> 8) & 511) < 256) {
+          const uint32_t cl = e[k] & 15;
+          r.bb >>= cl;
+          r.bc -= cl;
+          r.rel += cl;
+          if (r.bc <= 32) {
+            r.bb |= (uint64_t)w[k] << r.bc;
+            r.bc += 32;
+            ++r.q;
+          }
+        } else {
+          LaneBits t = lb;
+          t.q = r.q;
+          t.bb = r.bb;
+          t.bc = r.bc;
+          t.rel = r.rel;
+          uint32_t tk, nb;
+          const int rr = lane_token(t, lt, dt, tk, nb);
+          t.refill();
+          r.q = t.q;
+          r.bb = t.bb;
+          r.bc = t.bc;
+          r.rel = t.rel;
+          if (rr != 0) {
+            r.act = false;
+            continue;
+          }
+        }
+        if (r.rel > limit) {
+          r.act = false;
+        } else if (r.rel >= s_next) {
+          const uint32_t dd = r.rel - s_next;
+          r.ph = dd < 15 ? dd : 15;
+          r.act = false;
         }
       }
     }
-    map = (map & ~(0xFull << (4 * x))) | ((uint64_t)ph << (4 * x));
+#pragma unroll
+    for (int k = 0; k < PM_N; ++k)
+      if (x0 + k < xmax) map = (map & ~(0xFull << (4 * (x0 + k)))) | ((uint64_t)d[k].ph << (4 * (x0 + k)));
   }
   return map;
 }
@@ -376,7 +448,8 @@ __device__ __forceinline__ uint64_t compose_maps(uint64_t a, uint64_t b) {
 // wave per SIMD, 3 -> 2, and its units start mid-block anyway)
 #ifdef ZT_TK_TIME
 // debug: SIMT body decode cycles (lane 0 of each wave): [0] staging, [1] pass 1,
-// [2] repairs, [3] pass 2, [4] rounds, [5] repair iterations
+// [2] repairs (phase maps included), [3] pass 2, [4] rounds, [5] repair iterations,
+// [6] phase maps + their scan, [7] rounds that built phase maps
 __device__ unsigned long long g_tk_time[8];
 #define TK_T(v) v = __builtin_readcyclecounter()
 #else
@@ -404,6 +477,10 @@ __device__ int tok_huffman_simt(Reader &rd, uint64_t b0, const HuffTab *lt, cons
   for (;;) {
     [[maybe_unused]] unsigned long long tt0 = 0, tt1 = 0, tt2 = 0, tt3 = 0, tt4 = 0;
     [[maybe_unused]] int n_iter = 0;
+    [[maybe_unused]] unsigned long long tph = 0;
+#ifndef ZT_NO_PHASE_MAPS
+    uint64_t pmap = 0;  // fixedish: this round's phase map of the lane
+#endif
     TK_T(tt0);
     // ---- stage the round's input: bytes [a0, a0 + SP_STAGE_BYTES)
     const uint64_t a0 = ((b0 + R) >> 3) & ~uint64_t(15);
@@ -436,6 +513,36 @@ __device__ int tok_huffman_simt(Reader &rd, uint64_t b0, const HuffTab *lt, cons
     bool todo = in_range;
     uint32_t from = s_l;             // where this lane's current decode starts
     bool repair = false;
+#ifndef ZT_NO_PHASE_MAPS
+    if (PHASE && fixedish) {
+      // near-fixed-length codes: every lane's true start from the composed
+      // phase maps at once, instead of a speculative first pass that does not
+      // resynchronise on them; the first decode below is then each lane's
+      // true path (lanes whose start is unknown wait, as in the repairs)
+#ifdef ZT_TK_TIME
+      unsigned long long tp0;
+      TK_T(tp0);
+#endif
+      pmap = lane_phase_map(lb, b0, s_l, limit, in_range, 16u, lt, dt);
+      uint64_t P = pmap;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)P, d, 64);
+        const uint32_t hi = (uint32_t)__shfl_up((int)(uint32_t)(P >> 32), d, 64);
+        const uint64_t q = ((uint64_t)hi << 32) | lo;
+        if (lane >= d) P = compose_maps(P, q);
+      }
+      const uint32_t ph = lane == 0 ? 0u : ((uint32_t)__shfl_up((int)(uint32_t)P, 1, 64) & 15u);
+      todo = in_range && ph < 15;
+      from = s_l + ph;
+      repair = true;  // (the bitmap is empty: nothing to merge with)
+#ifdef ZT_TK_TIME
+      unsigned long long tp1;
+      TK_T(tp1);
+      tph += tp1 - tp0;
+#endif
+    }
+#endif
     for (int iter = 0;; ++iter) {
       if (iter > 66) return ZT_E_INPUT_BROKEN;
       bool active = todo;
@@ -517,13 +624,19 @@ __device__ int tok_huffman_simt(Reader &rd, uint64_t b0, const HuffTab *lt, cons
       if (f == 64) break;  // every lane synchronised, the block continues
       if (!__builtin_amdgcn_readlane((int)in_range, f)) return ZT_E_INPUT_BROKEN;  // runs past the input
 #ifndef ZT_NO_PHASE_MAPS
-      // (text regions of such a block repair a few lanes cheaply: maps only
-      // when many lanes missed)
-      if (PHASE && fixedish && iter == 0 && __popcll(U) >= 8) {
-        // every lane's true start from the composed phase maps; lanes whose
-        // start is unknown (a path ends or breaks before them) wait for the
-        // ordinary repairs, and the block's end is found as usual
-        uint64_t P = lane_phase_map(lb, b0, s_l, limit, in_range, lt, dt);
+      // Phase maps: lanes below f are on the true path and lane f's true
+      // start t_f is exact; every later lane's start comes from the maps
+      // composed from t_f's phase (lane f - 1's map replaced by that
+      // constant).  A lane whose start is unknown (a token 15 or more bits
+      // past a lane start, or a path that ends or breaks before it) waits:
+      // once the lanes before it are repaired it becomes lane f, and the maps
+      // carry on from there -- one iteration per such lane, where the
+      // ordinary repairs fixed one lane per iteration from it on.
+      if (PHASE && fixedish && f > 0) {
+        const uint32_t tf = __builtin_amdgcn_readlane(t, f);
+        const uint32_t sf = R + (uint32_t)f * SP_LANE_BITS;
+        const uint32_t phf = (tf >= sf && tf - sf < 15) ? tf - sf : 15u;
+        uint64_t P = lane == f - 1 ? 0x1111111111111111ull * phf : pmap;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
           const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)P, d, 64);
@@ -531,13 +644,18 @@ __device__ int tok_huffman_simt(Reader &rd, uint64_t b0, const HuffTab *lt, cons
           const uint64_t q = ((uint64_t)hi << 32) | lo;
           if (lane >= d) P = compose_maps(P, q);
         }
-        const uint32_t plo = (uint32_t)__shfl_up((int)(uint32_t)P, 1, 64);
-        const uint32_t ph = lane == 0 ? 0u : (plo & 15u);  // (map_{l-1} o ... o map_0)[0]
-        const bool known = in_range && ph < 15;
-        const uint32_t tt = (lane == 0 ? R : s_l) + ph;
-        const bool marked = known && ((sp->bm[ph >> 5][lane] >> (ph & 31)) & 1);
-        todo = known && !marked;
-        if (todo) from = tt;
+        const uint32_t ph = (uint32_t)__shfl_up((int)(uint32_t)P, 1, 64) & 15u;  // (map_{l-1} o ... o map_0)[0]
+        if (lane < f) {
+          todo = false;
+        } else if (lane == f) {
+          todo = in_range && t >= s_l && tp < SP_LANE_BITS;
+          from = t;
+        } else {
+          const bool known = in_range && ph < 15;
+          const bool marked = known && ((sp->bm[ph >> 5][lane] >> (ph & 31)) & 1);
+          todo = known && !marked;
+          from = s_l + ph;
+        }
         repair = true;
         continue;
       }
@@ -694,6 +812,8 @@ __device__ int tok_huffman_simt(Reader &rd, uint64_t b0, const HuffTab *lt, cons
       atomicAdd(&g_tk_time[3], tt4 - tt3);
       atomicAdd(&g_tk_time[4], 1ull);
       atomicAdd(&g_tk_time[5], (unsigned long long)n_iter);
+      atomicAdd(&g_tk_time[6], tph);
+      if (tph) atomicAdd(&g_tk_time[7], 1ull);
     }
 #endif
     if (eob) {

@@ -107,6 +107,8 @@ int get_ctx(DeviceCtx **out) {
     crc_shift_tables(x2n, shift);
     ZT_HIP(hipMalloc(&c->d_crc_shift, sizeof shift));
     ZT_HIP(hipMemcpy(c->d_crc_shift, shift, sizeof shift, hipMemcpyHostToDevice));
+    ZT_HIP(hipMalloc(&c->d_ck_acc, sizeof(CkAcc)));
+    ZT_HIP(hipMemset(c->d_ck_acc, 0, sizeof(CkAcc)));
     for (auto &e : c->ev) ZT_HIP(hipEventCreate(&e));
     g_ctx[g_dev] = c;
   }

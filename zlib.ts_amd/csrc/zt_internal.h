@@ -30,6 +30,12 @@ int hip_fail(hipError_t e, const char *what);
   } while (0)
 
 // ---- per-device context -----------------------------------------------------
+// checksum_segments' in-kernel merge (checksum.hip): zero between calls
+struct CkAcc {
+  unsigned long long s1, s2;
+  uint32_t crc, done;
+};
+
 // One default stream per device plus grow-only scratch buffers, so the
 // host-pointer entry points do not hipMalloc on every call.
 struct DeviceCtx {
@@ -44,6 +50,7 @@ struct DeviceCtx {
   uint32_t *d_crc_nib = nullptr;    // nibble tables (ZT_CRC_NIB_N entries)
   uint32_t *d_crc_x2n = nullptr;    // x^(2^k) mod P, k = 0..31
   uint32_t *d_crc_shift = nullptr;  // checksum.hip merge constants (crc_shift_tables)
+  CkAcc *d_ck_acc = nullptr;        // checksum merge accumulators (zeroed once, left zeroed by every call)
   // scratch
   void *d_buf[22] = {};  // slot 8: checksum segment partials; 10-17: general inflate (inflate_gen.hip);
                          // 20: segment inflate's sync-point sort (inflate_seg.hip); 21: stored runs
