@@ -22,5 +22,5 @@ for k, v in sorted(agg.items(), key=lambda kv: -kv[1]['SQ_WAVE_CYCLES'])[:10]:
     print(k[:22].ljust(22), " ".join(f"{c.replace('SQ_','')}={v[c]:.4g}" for c in sorted(v)))
 PY
 cat gpurun_out/$TAG/sq1.txt gpurun_out/$TAG/sq2.txt
-ZT_LIB=$R/zlib.ts_amd/build/var_dftime/libzt.so timeout -k 10 180 python3 tools/df_time.py wordsalad xorshift32 structured source > gpurun_out/$TAG/df_time.log 2>&1
+ZT_LIB=$R/zlib.ts_amd/build/var_dftime/libzt.so timeout -k 10 180 python3 tools/df_time.py wordsalad xorshift32 structured mixed > gpurun_out/$TAG/df_time.log 2>&1
 cat gpurun_out/$TAG/df_time.log

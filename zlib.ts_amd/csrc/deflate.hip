@@ -717,8 +717,10 @@ __device__ __forceinline__ void walk_pair_step(Walk &a, Walk &b, const MatchShar
   if ((threadIdx.x & 63) == 0) atomicAdd(&g_df_count[0], 1ull);
   atomicAdd(&g_df_count[1], (unsigned long long)(ha ? 1 : 0) + (hb ? 1 : 0));
 #endif
-  const bool ca = ha && ((oa ^ a.pw) & a.omask) == 0;
-  const bool cb = hb && ((ob ^ b.pw) & b.omask) == 0;
+  // (& not &&: a short-circuit lets the compiler sink a filter read into a
+  // branch, behind the other walk's wait)
+  const bool ca = ha & (((oa ^ a.pw) & a.omask) == 0);
+  const bool cb = hb & (((ob ^ b.pw) & b.omask) == 0);
   a.link = la;
   b.link = lb;
   a.active = ha && la != 0 && step + 1 < a.max_hops;
