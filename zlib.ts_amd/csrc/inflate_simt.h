@@ -840,7 +840,7 @@ constexpr uint32_t RS_AHEAD = ZT_RS_AHEAD;        // chunks in flight ahead of t
 static_assert((RS_AHEAD + 2) * 64 <= RS_TOK_RING, "expand token ring");
 constexpr uint32_t RS_FLUSH = 8192;           // output flush granule
 #ifndef ZT_CP_STEP
-#define ZT_CP_STEP 512
+#define ZT_CP_STEP 1024  // 512: copy_kernel 1.063 ms, expand 2.063 ms per GiB; 1024: 0.840 / 2.088 (profiles/r04cp_*)
 #endif
 constexpr uint32_t CP_STEP = ZT_CP_STEP;  // copy_kernel bytes per step (a multiple of 256)
 constexpr int CP_G = CP_STEP / 256;       // 4-byte groups per lane per step
