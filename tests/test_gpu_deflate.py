@@ -286,3 +286,62 @@ def test_device_stream_at_unaligned_output(zt, oracle, shift):
     assert la == lu and u[shift:shift + lu] == a
     assert u[:shift] == b"\xa5" * shift and u[shift + lu] == 0xA5  # neighbours untouched
     assert zlib.decompress(a, -15) == d
+
+
+def _plan_inflate(zt, s, cap):
+    import torch
+
+    di = torch.frombuffer(bytearray(s), dtype=torch.uint8).cuda()
+    do = torch.full((cap + 64,), 0x5A, dtype=torch.uint8, device="cuda")
+    p = zt.InflatePlan(len(s), cap)
+    try:
+        olen, eip = p.run(di.data_ptr(), len(s), do.data_ptr(), cap)
+    finally:
+        p.close()
+    torch.cuda.synchronize()
+    return olen, eip, do.cpu().numpy().tobytes()
+
+
+def test_device_chain(zt, oracle):
+    """zt_inflate_dev into a caller's buffer builds the unit chain, the copy
+    segments and their descriptor offsets on the device (chain_kernel) when
+    every unit follows the one before -- text, stored runs (classify_kernel's
+    random windows: direct segments), restart markers, ragged end -- and the
+    bytes past the output stay untouched."""
+    d = b"".join([oracle.gen("wordsalad", 41, (3 << 20) + 5), oracle.gen("xorshift32", 41, (2 << 20) + 3),
+                  oracle.gen("structured", 41, (1 << 20) + 1), b"\0" * 70001, oracle.gen("wordsalad", 42, 12345)])
+    s = zt.deflate_raw(d)
+    zt.timing_enable(True)
+    olen, eip, out = _plan_inflate(zt, s, len(d) + 1000)
+    t = zt.timing_read()
+    zt.timing_enable(False)
+    assert t["inflate_toks"] == 1, "the two-phase inflate did not run"
+    assert olen == len(d) and eip == len(s)
+    assert out[:olen] == d and out[olen:olen + 64] == b"\x5a" * 64
+    # the same stream through the host API (host-built chain)
+    assert zt.inflate_raw(s) == (d, len(s))
+
+
+def test_device_chain_falls_back(zt, oracle):
+    """Streams the device chain does not take -- false sync-point candidates
+    inside stored data, an output capacity below the stream's size -- give
+    the host walk's results."""
+    pat = b"\0\0\0\xff\xff\0\0\0\xff\xff"
+    d = oracle.gen("wordsalad", 4, 1 << 19) + pat * 40000 + oracle.gen("xorshift32", 4, 1 << 19)
+    s = zt.deflate_raw(d)
+    olen, eip, out = _plan_inflate(zt, s, len(d) + 100)
+    assert olen == len(d) and eip == len(s) and out[:olen] == d
+    chunk = bytearray(oracle.gen("xorshift32", 9, 65535))
+    chunk[-10:] = pat
+    chunk[1000:1010] = pat
+    d2 = bytes(chunk) * 8
+    s2 = zt.deflate_raw(d2, compression_type=0)
+    olen, eip, out = _plan_inflate(zt, s2, len(d2))
+    assert olen == len(d2) and out[:olen] == d2
+    # capacity one byte short
+    d3 = oracle.gen("wordsalad", 5, 3 << 20)
+    s3 = zt.deflate_raw(d3)
+    with pytest.raises(zt.ZtError):
+        _plan_inflate(zt, s3, len(d3) - 1)
+    olen, eip, out = _plan_inflate(zt, s3, len(d3))
+    assert olen == len(d3) and out[:olen] == d3

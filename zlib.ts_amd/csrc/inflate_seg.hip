@@ -34,6 +34,7 @@
 
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
+#include <rocprim/warp/warp_scan.hpp>
 
 #include "zt_internal.h"
 
@@ -196,7 +197,7 @@ __global__ __launch_bounds__(256) void unit_jobs(const uint64_t *__restrict__ ke
                                                  const uint32_t *__restrict__ pos, uint32_t cnt, uint64_t n,
                                                  uint64_t index, uint32_t cap, uint64_t *__restrict__ sync,
                                                  uint8_t *__restrict__ restart, TokJob *__restrict__ jobs,
-                                                 uint64_t *__restrict__ slot) {
+                                                 uint64_t *__restrict__ slot, uint32_t *__restrict__ nrestart) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   auto job = [&](uint32_t u, uint64_t start, uint64_t next) {
     TokJob j;
@@ -217,6 +218,7 @@ __global__ __launch_bounds__(256) void unit_jobs(const uint64_t *__restrict__ ke
   while (j < cnt && (key[j] >> 1) == p) ++j;
   sync[k] = p;
   restart[k] = (uint8_t)(key[i] & 1);
+  if (key[i] & 1) atomicAdd(nrestart, 1u);
   job(k + 1, p, j < cnt ? key[j] >> 1 : n);
 }
 
@@ -232,6 +234,257 @@ __global__ __launch_bounds__(256) void unit_slots(const uint64_t *__restrict__ o
 }
 
 }  // namespace
+
+// ---- the chain on the device (the common case) --------------------------------
+// When every unit is on the chain in order -- unit u stops at sync point u and
+// the last one at BFINAL, i.e. no false sync-point candidate -- the chain, its
+// copy segments and their descriptor offsets are prefix sums, and one
+// workgroup builds them where the host walk needed every unit's result back
+// over PCIe and the chain sent down again (a host round trip between tokenize
+// and expand).  Anything else (a false candidate, a unit error, an output past
+// the capacity, more segments than the bound) leaves info->ok = 0: expand and
+// copy return at once and the host walks the chain as before.  Segment rules
+// as the host walk's: a segment starts at unit 0 and at the first unit after
+// a restart point that has output bytes since the previous restart point
+// (empty segments merge into the next); its descriptors start 512-aligned; a
+// segment of stored runs only is copied by expand_kernel (SegJob count bit 31).
+constexpr int CH_T = 1024;
+constexpr uint32_t CH_MAXU = 40960;  // units (LDS: 2 B each): 1.25 GiB of 32 KiB blocks
+constexpr int CH_B = 8;              // rounds whose loads are in flight together
+constexpr uint32_t CH_MAXS = 2048;   // segments (LDS)
+
+__device__ __forceinline__ uint64_t shfl_up64(uint64_t v, int d) {
+  const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)v, d, 64);
+  const uint32_t hi = (uint32_t)__shfl_up((int)(uint32_t)(v >> 32), d, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+struct AddU64 {
+  __device__ uint64_t operator()(uint64_t a, uint64_t b) const { return a + b; }
+};
+struct MaxU64 {
+  __device__ uint64_t operator()(uint64_t a, uint64_t b) const { return a > b ? a : b; }
+};
+// exclusive scan over the workgroup's CH_T threads (identity 0); *total = the reduction
+template <typename Op>
+__device__ uint64_t block_excl_scan(uint64_t v, Op op, uint64_t *wsum, uint64_t *total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint64_t x = v;
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t y = shfl_up64(x, d);
+    if (lane >= d) x = op(x, y);
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  if (w == 0) {
+    uint64_t sw = lane < CH_T / 64 ? wsum[lane] : 0;
+    for (int d = 1; d < CH_T / 64; d <<= 1) {
+      const uint64_t y = shfl_up64(sw, d);
+      if (lane >= d) sw = op(sw, y);
+    }
+    if (lane < CH_T / 64) wsum[lane] = sw;
+  }
+  __syncthreads();
+  uint64_t ex = shfl_up64(x, 1);
+  if (lane == 0) ex = 0;
+  const uint64_t r = op(w ? wsum[w - 1] : 0, ex);
+  if (total) *total = wsum[CH_T / 64 - 1];
+  __syncthreads();
+  return r;
+}
+
+// wave w owns units [w * wu, (w + 1) * wu), taken 64 at a time (lane = unit:
+// every global access coalesced); running values cross rounds in registers
+// and waves through one workgroup scan
+__global__ __launch_bounds__(CH_T) void chain_kernel(const TokResult *__restrict__ res, const uint8_t *__restrict__ restart,
+                                                     const uint64_t *__restrict__ tok_off, uint32_t units,
+                                                     uint64_t out_cap, uint64_t desc_cap, uint32_t max_seg,
+                                                     ChainUnit *__restrict__ cu, SegJob *__restrict__ sj,
+                                                     ChainInfo *__restrict__ info) {
+  __shared__ uint16_t ol[CH_MAXU];              // unit output bytes (<= 65535 here)
+  __shared__ uint32_t candb[CH_MAXU / 32];      // unit follows a restart point (or is unit 0)
+  __shared__ uint32_t dirb[CH_MAXU / 32];       // unit is stored runs only, or empty
+  __shared__ uint64_t seg_off[CH_MAXS + 1];     // output offset of segment k's first unit; [nseg] = total
+  __shared__ uint64_t seg_desc[CH_MAXS];
+  __shared__ uint32_t seg_first[CH_MAXS + 1];
+  __shared__ uint32_t seg_direct[CH_MAXS];
+  __shared__ uint64_t wsum[CH_T / 64];
+  __shared__ int bad;
+  const uint32_t t = threadIdx.x;
+  const int lane = t & 63;
+  const uint32_t w = t >> 6, nw = CH_T / 64;
+  const uint32_t wu = ((units + nw - 1) / nw + 63) & ~63u;  // units per wave, whole rounds
+  const uint32_t w0 = w * wu < units ? w * wu : units, w1 = w0 + wu < units ? w0 + wu : units;
+  if (t == 0) bad = 0;
+  for (uint32_t i = t; i < CH_MAXU / 32; i += CH_T) candb[i] = dirb[i] = 0;
+  for (uint32_t i = t; i < CH_MAXS; i += CH_T) seg_direct[i] = 1;
+  __syncthreads();
+  // A: the unit results into LDS (CH_B rounds' loads in flight); every unit
+  // on the chain in order; the wave's bytes
+  bool ok = true;
+  uint64_t wlen = 0;
+  for (uint32_t r0 = w0; r0 < w1; r0 += 64 * CH_B) {
+    uint64_t olen[CH_B];
+    int32_t st[CH_B], stop[CH_B];
+    uint32_t ntok[CH_B];
+    uint8_t rs[CH_B];
+#pragma unroll
+    for (int j = 0; j < CH_B; ++j) {
+      const uint32_t v = r0 + 64 * j + lane, u = v < w1 ? v : w0;
+      olen[j] = res[u].out_len;
+      st[j] = res[u].status;
+      stop[j] = res[u].stop_idx;
+      ntok[j] = res[u].ntok;
+      rs[j] = restart[u ? u - 1 : 0];
+    }
+#pragma unroll
+    for (int j = 0; j < CH_B; ++j) {
+      const uint32_t u = r0 + 64 * j + lane;
+      if (u >= w1) continue;
+      ok = ok && st[j] == ZT_OK && olen[j] <= 0xFFFFull && (u + 1 < units ? stop[j] == (int32_t)u : stop[j] < 0);
+      ol[u] = (uint16_t)olen[j];
+      wlen += olen[j];
+      if (u == 0 || rs[j] != 0) atomicOr(&candb[u >> 5], 1u << (u & 31));
+      if ((ntok[j] >> 30) == 3u || olen[j] == 0) atomicOr(&dirb[u >> 5], 1u << (u & 31));
+    }
+  }
+  if (!ok) bad = 1;
+  for (int o = 32; o; o >>= 1) wlen += ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(wlen >> 32), o, 64) << 32) |
+                                       (uint32_t)__shfl_xor((int)(uint32_t)wlen, o, 64);
+  uint64_t total;
+  const uint64_t wbase = block_excl_scan(lane == 0 ? wlen : 0, AddU64(), wsum, &total);  // (one lane per wave)
+  const uint64_t base = __shfl((int)(uint32_t)wbase, 0, 64) | ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(wbase >> 32), 0, 64) << 32);
+  auto cand = [&](uint32_t u) { return u < w1 && ((candb[u >> 5] >> (u & 31)) & 1u); };
+  // One round of 64 units: u's output offset o (the round's sums are 32-bit:
+  // units <= 65535 bytes), whether u starts a segment (a restart point with
+  // output since the previous one: pcr = that one's offset before the round),
+  // and the running values for the next round (wave scans by DPP, rocPRIM).
+  using WScan = rocprim::warp_scan<uint32_t, 64>;
+  __shared__ typename WScan::storage_type wst[CH_T / 64];
+  struct Round {
+    uint64_t o;
+    bool start;
+  };
+  auto round = [&](uint32_t u, uint32_t l, uint64_t &off, uint64_t &pcr) -> Round {
+    uint32_t inc;
+    WScan().inclusive_scan(l, inc, wst[w], rocprim::plus<uint32_t>());
+    const uint64_t o = off + inc - l;
+    const bool c = cand(u);
+    const uint32_t cv = c ? inc - l + 1 : 0u;  // 1 + the round-local offset of a restart point
+    uint32_t ex;
+    WScan().exclusive_scan(cv, ex, 0u, wst[w], rocprim::maximum<uint32_t>());
+    const uint64_t before = ex ? off + ex - 1 : pcr;
+    const uint32_t rmax = (uint32_t)__shfl((int)(ex > cv ? ex : cv), 63, 64);
+    const bool start = u < w1 && (u == 0 || (c && o > before));
+    if (rmax) pcr = off + rmax - 1;
+    off += (uint32_t)__shfl((int)inc, 63, 64);
+    return Round{o, start};
+  };
+  // B: output offset of the wave's last restart point (non-decreasing: a max-scan)
+  uint64_t off = base, last = 0;
+  for (uint32_t r0 = w0; r0 < w1; r0 += 64) {
+    const uint32_t u = r0 + lane;
+    (void)round(u, u < w1 ? ol[u] : 0u, off, last);
+  }
+  const uint64_t prevw = block_excl_scan(lane == 0 ? last : 0, MaxU64(), wsum, nullptr);
+  const uint64_t prev = __shfl((int)(uint32_t)prevw, 0, 64) | ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(prevw >> 32), 0, 64) << 32);
+  // C: segment starts per wave
+  uint64_t nstart = 0, pc = prev;
+  off = base;
+  for (uint32_t r0 = w0; r0 < w1; r0 += 64) {
+    const uint32_t u = r0 + lane;
+    const Round r = round(u, u < w1 ? ol[u] : 0u, off, pc);
+    nstart += __popcll(__ballot(r.start));
+  }
+  uint64_t nseg64;
+  const uint64_t sbw = block_excl_scan(lane == 0 ? nstart : 0, AddU64(), wsum, &nseg64);
+  const uint32_t sbase = (uint32_t)__shfl((int)(uint32_t)sbw, 0, 64);
+  const uint32_t nseg = (uint32_t)nseg64;
+  if (bad || total > out_cap || nseg > max_seg || nseg > CH_MAXS) {
+    if (t == 0) info->ok = 0;
+    return;  // (uniform: bad was set before the scans' barriers)
+  }
+  // D: the segment table; a segment is direct when all its units are stored runs (or empty)
+  uint32_t k = sbase;  // segments started before this round
+  pc = prev;
+  off = base;
+  for (uint32_t r0 = w0; r0 < w1; r0 += 64) {
+    const uint32_t u = r0 + lane;
+    const Round r = round(u, u < w1 ? ol[u] : 0u, off, pc);
+    const uint64_t sm = __ballot(r.start);
+    const uint32_t g = k + (uint32_t)__popcll(sm & ((2ull << lane) - 1)) - 1;  // this unit's segment
+    if (r.start) {
+      seg_first[g] = u;
+      seg_off[g] = r.o;
+    }
+    if (u < w1 && !((dirb[u >> 5] >> (u & 31)) & 1)) seg_direct[g] = 0;
+    k += (uint32_t)__popcll(sm);
+  }
+  if (t == 0) {
+    seg_first[nseg] = units;
+    seg_off[nseg] = total;
+  }
+  __syncthreads();
+  // E: descriptor offsets, each segment 512-aligned
+  const uint32_t sper = (nseg + CH_T - 1) / CH_T;
+  const uint32_t s0 = t * sper < nseg ? t * sper : nseg, s1 = s0 + sper < nseg ? s0 + sper : nseg;
+  uint64_t dl = 0;
+  for (uint32_t q = s0; q < s1; ++q) dl += (seg_off[q + 1] - seg_off[q] + 511) & ~uint64_t(511);
+  uint64_t db = block_excl_scan(dl, AddU64(), wsum, nullptr);
+  for (uint32_t q = s0; q < s1; ++q) {
+    seg_desc[q] = db;
+    db += (seg_off[q + 1] - seg_off[q] + 511) & ~uint64_t(511);
+  }
+  __syncthreads();
+  const uint64_t desc_total = seg_desc[nseg - 1] + (total - seg_off[nseg - 1]);
+  if (desc_total + 1024 > desc_cap) {
+    if (t == 0) info->ok = 0;
+    return;  // (uniform)
+  }
+  // F: chain units (coalesced) and segment jobs
+  k = sbase;
+  pc = prev;
+  off = base;
+  for (uint32_t b0 = w0; b0 < w1; b0 += 64 * CH_B) {
+    uint64_t to[CH_B];
+    uint32_t nt[CH_B];
+#pragma unroll
+    for (int j = 0; j < CH_B; ++j) {  // CH_B rounds' loads in flight (each round waited alone: 0.1 ms)
+      const uint32_t v = b0 + 64 * j + lane, uu = v < w1 ? v : w0;
+      to[j] = tok_off[uu];
+      nt[j] = res[uu].ntok;
+    }
+#pragma unroll
+    for (int j = 0; j < CH_B; ++j) {
+      const uint32_t r0 = b0 + 64 * j;
+      if (r0 >= w1) break;  // (wave-uniform)
+      const uint32_t u = r0 + lane;
+      const uint32_t l = u < w1 ? ol[u] : 0u;
+      const Round r = round(u, l, off, pc);
+      const uint64_t sm = __ballot(r.start);
+      const uint32_t g = k + (uint32_t)__popcll(sm & ((2ull << lane) - 1)) - 1;
+      if (u < w1) {
+        ChainUnit x;
+        x.tok_off = to[j];
+        x.out_off = r.o;
+        x.seg_off = seg_off[g];
+        x.desc_off = seg_desc[g] + (r.o - seg_off[g]);
+        x.ntok = seg_direct[g] ? nt[j] : (nt[j] & ~0x40000000u);
+        x.out_len = l;
+        cu[u] = x;
+      }
+      k += (uint32_t)__popcll(sm);
+    }
+  }
+  for (uint32_t q = t; q < nseg; q += CH_T)
+    sj[q] = SegJob{seg_first[q], (seg_first[q + 1] - seg_first[q]) | (seg_direct[q] ? 0x80000000u : 0u)};
+  if (t == 0) {
+    info->ok = 1;
+    info->nseg = nseg;
+    info->total = total;
+    info->end_bits = res[units - 1].end_bits;
+    info->desc_total = desc_total;
+  }
+}
 
 // ZT_INF_TIMING=1: host wall time of inflate_segments_dev's stages on stderr (measurement only)
 static double it_now() {
@@ -305,14 +558,17 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   TokResult *d_res =
       reinterpret_cast<TokResult *>(static_cast<uint8_t *>(d_meta) + stops_bytes + restart_bytes + jobs_bytes);
   ZT_HIP(hipMemsetAsync(d_slot, 0, units_max * 8, s));
-  unit_jobs<<<g, 256, 0, s>>>(d_key, d_flag, d_pos, cnt, n, index, kUnitTokCap, d_stops, d_restart, d_jobs, d_slot);
+  ZT_HIP(hipMemsetAsync(d_ttot + 2, 0, 8, s));
+  unit_jobs<<<g, 256, 0, s>>>(d_key, d_flag, d_pos, cnt, n, index, kUnitTokCap, d_stops, d_restart, d_jobs, d_slot,
+                              reinterpret_cast<uint32_t *>(d_ttot + 2));
   ZT_HIP(hipGetLastError());
   ZT_HIP(rocprim::exclusive_scan(sb, t_scan64, d_slot, d_off, (uint64_t)0, units_max, rocprim::plus<uint64_t>(), s));
   unit_slots<<<g, 256, 0, s>>>(d_off, d_slot, d_pos + cnt, d_jobs, d_ttot);
   ZT_HIP(hipGetLastError());
-  uint64_t tot_h[2] = {0, 0};
+  uint64_t tot_h[3] = {0, 0, 0};
   ZT_HIP(hipMemcpyAsync(&tot_h[0], d_ttot, 8, hipMemcpyDeviceToHost, s));
   ZT_HIP(hipMemcpyAsync(&tot_h[1], d_pos + cnt, 4, hipMemcpyDeviceToHost, s));
+  ZT_HIP(hipMemcpyAsync(&tot_h[2], d_ttot + 2, 4, hipMemcpyDeviceToHost, s));
   ZT_HIP(hipStreamSynchronize(s));
   IT("units counted");
   const uint32_t nsync = (uint32_t)tot_h[1];
@@ -366,6 +622,67 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   ZT_TRY(timing_begin(c, s, 3));
   ZT_TRY(tokenize_units_dev(tp, s));
   ZT_TRY(timing_end(c, s, 3));
+  // 3a. the common case: chain, segments and the resolve kernels straight on
+  // the device (a caller-owned output: its capacity bounds the descriptors);
+  // ZT_INF_HOST_CHAIN=1 forces the host walk (measurement)
+  static const bool host_chain = getenv("ZT_INF_HOST_CHAIN") != nullptr;
+  const uint32_t max_seg = (uint32_t)std::min<uint64_t>(tot_h[2] + 1, units);
+  const uint64_t desc_cap = (uint64_t)out_cap + 512ull * max_seg + 2048;
+  if (*d_out_io && !check && !inf_debug() && !host_chain && max_seg <= CH_MAXS && units <= CH_MAXU &&
+      out_cap <= (64ull << 30)) {
+    void *d_chain, *d_desc;
+    const size_t chain_bytes = align256(units * sizeof(ChainUnit)), seg_bytes = align256(max_seg * sizeof(SegJob));
+    const size_t ust_bytes = align256(units * 4), st_bytes = align256(max_seg * 4);
+    ZT_TRY(scratch(c, 7, chain_bytes + seg_bytes + ust_bytes + st_bytes + 256, &d_chain));
+    ZT_TRY(scratch(c, 3, desc_cap * 2, &d_desc));
+    uint8_t *cb = static_cast<uint8_t *>(d_chain);
+    ChainUnit *d_cu = reinterpret_cast<ChainUnit *>(cb);
+    SegJob *d_sj = reinterpret_cast<SegJob *>(cb + chain_bytes);
+    int32_t *d_ust = reinterpret_cast<int32_t *>(cb + chain_bytes + seg_bytes);
+    int32_t *d_st = reinterpret_cast<int32_t *>(cb + chain_bytes + seg_bytes + ust_bytes);
+    ChainInfo *d_info = reinterpret_cast<ChainInfo *>(cb + chain_bytes + seg_bytes + ust_bytes + st_bytes);
+    chain_kernel<<<1, CH_T, 0, s>>>(d_res, d_restart, d_off, (uint32_t)units, out_cap, desc_cap, max_seg, d_cu, d_sj,
+                                    d_info);
+    ZT_HIP(hipGetLastError());
+    ResolveParams rp;
+    rp.tokens = static_cast<const uint32_t *>(d_tok);
+    rp.units = d_cu;
+    rp.segs = d_sj;
+    rp.out = *d_out_io;
+    rp.desc = static_cast<uint16_t *>(d_desc);
+    rp.unit_status = d_ust;
+    rp.seg_status = d_st;
+    rp.nunits = (uint32_t)units;
+    rp.nseg = max_seg;  // (grid; copy waves past info->nseg return at once)
+    rp.marker = 0;
+    rp.in = d_in;
+    rp.info = d_info;
+    IT("device chain launched");
+    ZT_TRY(resolve_segments_dev(rp, s));
+    ZT_TRY(timing_end(c, s, 2));
+    // back in one copy: the chain summary and every status
+    uint8_t *hb = pin + meta_a;
+    ZT_HIP(hipMemcpyAsync(hb, d_ust, ust_bytes + st_bytes + sizeof(ChainInfo), hipMemcpyDeviceToHost, s));
+    ZT_HIP(hipStreamSynchronize(s));
+    IT("resolved (device chain)");
+    const ChainInfo info = *reinterpret_cast<const ChainInfo *>(hb + ust_bytes + st_bytes);
+    if (info.ok) {
+      ZT_TRY(timing_collect(c, &c->times.inflate_ms, &c->times.inflate_launches, 2));
+      ZT_TRY(timing_collect(c, &c->times.inflate_tok_ms, &c->times.inflate_toks, 3));
+      const int32_t *h_ust = reinterpret_cast<const int32_t *>(hb);
+      const int32_t *h_st = reinterpret_cast<const int32_t *>(hb + ust_bytes);
+      for (size_t i = 0; i < units; ++i)
+        if (h_ust[i] != ZT_OK) FALLBACK("unit %zu of %zu (device chain): status %d\n", i, units, h_ust[i]);
+      for (size_t i = 0; i < info.nseg; ++i)
+        if (h_st[i] != ZT_OK) FALLBACK("segment %zu of %u: status %d\n", i, info.nseg, h_st[i]);
+      *out_len = info.total;
+      *end_ip = (info.end_bits + 7) >> 3;
+      c->times.inflate_paths[0]++;
+      return ZT_OK;
+    }
+    // not the common case: the host walks the chain (the kernels above did nothing)
+    ZT_TRY(timing_begin(c, s, 2));
+  }
   TokResult *res = reinterpret_cast<TokResult *>(pin + restart_bytes);
   ZT_HIP(hipMemcpyAsync(pin, d_restart, nsync, hipMemcpyDeviceToHost, s));
   ZT_HIP(hipMemcpyAsync(res, d_res, units * sizeof(TokResult), hipMemcpyDeviceToHost, s));

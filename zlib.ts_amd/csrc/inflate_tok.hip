@@ -445,6 +445,7 @@ __device__ __forceinline__ void expand_direct(const ResolveParams &P, const Chai
 
 __global__ __launch_bounds__(64) void expand_kernel(ResolveParams P) {
   __shared__ ExpandShared sh;
+  if (P.info && !P.info->ok) return;  // the host walks the chain instead
   const ChainUnit cu = P.units[blockIdx.x];
   if ((cu.ntok >> 30) == 3u)
     expand_direct(P, cu);
@@ -506,6 +507,8 @@ __global__ __launch_bounds__(64) void copy_kernel(ResolveParams P) {
 #endif
   const uint32_t sg = blockIdx.x;
   const int lane = threadIdx.x & 63;
+  // device-built chain: launched for the bound on its segments
+  if (P.info && (!P.info->ok || sg >= P.info->nseg)) return;
   SegJob sj = P.segs[sg];
   if (sj.count >> 31) {  // stored runs only: expand_kernel wrote the bytes
     if (lane == 0) P.seg_status[sg] = ZT_OK;

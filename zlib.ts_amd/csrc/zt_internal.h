@@ -257,6 +257,15 @@ struct ChainUnit {
 struct SegJob {
   uint32_t first, count;  // chain units [first, first + count)
 };
+// the chain built on the device (inflate_seg.hip chain_kernel); ok == 0: not
+// the common case, expand / copy return at once and the host walks the chain
+struct ChainInfo {
+  int32_t ok;
+  uint32_t nseg;
+  uint64_t total;       // output bytes
+  uint64_t end_bits;    // bit after the last unit's last block
+  uint64_t desc_total;  // descriptors
+};
 struct ResolveParams {
   const uint32_t *tokens;
   const ChainUnit *units;
@@ -269,6 +278,7 @@ struct ResolveParams {
   uint32_t nseg;
   int32_t marker;        // expand: segments after the first may reach up to 32 KiB behind their start
   const uint8_t *in;     // expand: the compressed input (payloads of run tokens)
+  const ChainInfo *info = nullptr;  // device-built chain: nothing to do unless info->ok; nseg = info->nseg
 };
 int tokenize_units_dev(const TokParams &p, hipStream_t s);
 int resolve_segments_dev(const ResolveParams &p, hipStream_t s);
