@@ -1,8 +1,7 @@
 #!/bin/bash
-# Round checkpoint on one GPU box: full GPU tests, smoke, PMC HBM traffic of
-# the bench workload (FETCH_SIZE, read requests by size, WRITE_SIZE in separate passes ->
-# profiles/pmc_traffic.json, which bench.py reports as roofline.traffic),
-# the bench line, and rocprofv3 kernel stats of the bench.
+# Round checkpoint on one GPU box: full GPU tests, smoke, the bench line,
+# rocprofv3 kernel stats of the bench and of C1 / C2 / C4 (the PMC HBM
+# traffic passes: tools/gpu_checkpoint_pmc.sh).
 #   usage: tools/gpu_checkpoint.sh TAG
 set -e
 TAG=${1:-ck}
@@ -13,13 +12,6 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 tail -1 gpurun_out/${TAG}_pytest.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1
 tail -1 gpurun_out/${TAG}_smoke.log
-cd /tmp
-timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE -f csv -d $R/gpurun_out/${TAG}_pmcf -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-api > $R/gpurun_out/${TAG}_pmcf.log 2>&1
-timeout -s KILL 180 rocprofv3 --pmc TCC_EA0_RDREQ_32B TCC_EA0_RDREQ_64B TCC_EA0_RDREQ_128B TCC_EA0_RDREQ_DRAM_32B -f csv -d $R/gpurun_out/${TAG}_pmcq -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-api > $R/gpurun_out/${TAG}_pmcq.log 2>&1
-timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE -f csv -d $R/gpurun_out/${TAG}_pmcw -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-api > $R/gpurun_out/${TAG}_pmcw.log 2>&1
-cd $R
-python3 tools/pmc_traffic.py profiles/pmc_traffic.json gpurun_out/${TAG}_pmcf gpurun_out/${TAG}_pmcq gpurun_out/${TAG}_pmcw > gpurun_out/${TAG}_pmc.txt && cp profiles/pmc_traffic.json gpurun_out/${TAG}_pmc_traffic.json
-grep -E 'match_kernel|tokenize|copy_kernel|checksum' gpurun_out/${TAG}_pmc.txt || true
 timeout -k 10 600 python bench.py > gpurun_out/${TAG}_bench.log 2>&1
 tail -1 gpurun_out/${TAG}_bench.log
 cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d $R/gpurun_out/${TAG}_prof -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-api > $R/gpurun_out/${TAG}_prof.log 2>&1
