@@ -30,6 +30,6 @@ for par in (0, 1):
     zt.lib.zt_debug_tk_time(buf)
     r = max(1, buf[4])
     print(f"{c2_corpus.kind(idx[0]):10s} {count} streams, call {dt*1e3:.1f} ms: {buf[4]} rounds, "
-          f"{buf[5] / r:.2f} repair iterations per round, {buf[7]} with phase maps; cycles per round: "
-          f"stage {buf[0] / r:.0f}  pass1 {buf[1] / r:.0f}  repairs {buf[2] / r:.0f} (maps {buf[6] / r:.0f})  "
+          f"{buf[5] / r:.2f} repair iterations per round; cycles per round: "
+          f"stage {buf[0] / r:.0f} (store wait {buf[7] / r:.0f})  pass1 {buf[1] / r:.0f}  repairs {buf[2] / r:.0f} (maps {buf[6] / r:.0f})  "
           f"pass2 {buf[3] / r:.0f}", flush=True)

@@ -26,4 +26,4 @@ for kind in sys.argv[2:] or ["wordsalad", "structured", "mixed"]:
     assert torch.equal(d_out[:n], d_in[:n])
     r = max(1, buf[4])
     print(f"{kind:10s} {buf[4]} rounds, {buf[5] / r:.2f} repair iterations per round; cycles per round: "
-          f"stage {buf[0] / r:.0f}  pass1 {buf[1] / r:.0f}  repairs {buf[2] / r:.0f}  pass2 {buf[3] / r:.0f}", flush=True)
+          f"stage {buf[0] / r:.0f} (store wait {buf[7] / r:.0f})  pass1 {buf[1] / r:.0f}  repairs {buf[2] / r:.0f}  pass2 {buf[3] / r:.0f}", flush=True)

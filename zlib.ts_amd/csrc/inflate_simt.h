@@ -449,7 +449,7 @@ __device__ __forceinline__ uint64_t compose_maps(uint64_t a, uint64_t b) {
 #ifdef ZT_TK_TIME
 // debug: SIMT body decode cycles (lane 0 of each wave): [0] staging, [1] pass 1,
 // [2] repairs (phase maps included), [3] pass 2, [4] rounds, [5] repair iterations,
-// [6] phase maps + their scan, [7] rounds that built phase maps
+// [6] phase maps + their scan, [7] of [0]: waiting for the previous round's stores
 __device__ unsigned long long g_tk_time[8];
 #define TK_T(v) v = __builtin_readcyclecounter()
 #else
@@ -482,6 +482,13 @@ __device__ int tok_huffman_simt(Reader &rd, uint64_t b0, const HuffTab *lt, cons
     uint64_t pmap = 0;  // fixedish: this round's phase map of the lane
 #endif
     TK_T(tt0);
+#ifdef ZT_TK_TIME
+    // (measurement: the previous round's token stores, which the stage's
+    // loads wait for -- one vmcnt on gfx9)
+    unsigned long long ttw;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    TK_T(ttw);
+#endif
     // ---- stage the round's input: bytes [a0, a0 + SP_STAGE_BYTES)
     const uint64_t a0 = ((b0 + R) >> 3) & ~uint64_t(15);
     {
@@ -813,7 +820,7 @@ __device__ int tok_huffman_simt(Reader &rd, uint64_t b0, const HuffTab *lt, cons
       atomicAdd(&g_tk_time[4], 1ull);
       atomicAdd(&g_tk_time[5], (unsigned long long)n_iter);
       atomicAdd(&g_tk_time[6], tph);
-      if (tph) atomicAdd(&g_tk_time[7], 1ull);
+      atomicAdd(&g_tk_time[7], ttw - tt0);
     }
 #endif
     if (eob) {
