@@ -486,11 +486,46 @@ __device__ void load_sub(MatchShared *s, const uint8_t *g, uint32_t rel0, uint32
 // p held a position 32 KiB back, out of every walk's reach) and
 // link4[p % DF_SUB] (the previous sub-chunk's, whose searches are done).  The
 // serial link waves then only read them (chain_link).
+// Four consecutive positions per thread: three aligned dword reads (lanes on
+// consecutive words: no bank conflicts) give all four 8-byte keys by byte
+// aligns, and a full quad's hashes go out as one 8-byte store per table
+// (one position per thread took two unaligned reads -- two dwords each -- and
+// two 2-byte stores per position).  Slots outside [lo, hi) keep their values:
+// below lo are links already made, and link4's slots past hi are this
+// sub-chunk's first positions.
 __device__ __forceinline__ void hash_keys(MatchShared *s, uint32_t lo, uint32_t hi, Key key) {
+#ifdef ZT_DF_HASH1
   for (uint32_t p = lo + threadIdx.x; p < hi; p += DF_THREADS) {
     s->prev[ridx(p)] = (uint16_t)key_hash(s, p, key);
     s->link4[p & (DF_SUB - 1)] = (uint16_t)key4_hash(s, p);
   }
+#else
+  for (uint32_t p4 = (lo & ~3u) + 4 * threadIdx.x; p4 < hi; p4 += 4 * DF_THREADS) {
+    const uint32_t w = ridx(p4) >> 2;  // (the mirror past the ring's end holds w + 1, w + 2 at the wrap)
+    const uint32_t d0 = s->ring[w], d1 = s->ring[w + 1], d2 = s->ring[w + 2];
+    uint32_t hk[4], h4[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t x0 = k ? __builtin_amdgcn_alignbyte(d1, d0, k) : d0;
+      const uint32_t x1 = k ? __builtin_amdgcn_alignbyte(d2, d1, k) : d1;
+      const uint32_t v = (x0 & key.kmask) ^ ((x1 & key.kmask2) * 0x2545F491u);
+      hk[k] = __umulhi(v * 0x9E3779B1u, DF_HSIZE);
+      h4[k] = __umulhi(x0 * 0x9E3779B1u, DF_H4SIZE);
+    }
+    if (p4 >= lo && p4 + 4 <= hi) {
+      *reinterpret_cast<uint2 *>(&s->prev[ridx(p4)]) = make_uint2(hk[0] | hk[1] << 16, hk[2] | hk[3] << 16);
+      *reinterpret_cast<uint2 *>(&s->link4[p4 & (DF_SUB - 1)]) = make_uint2(h4[0] | h4[1] << 16, h4[2] | h4[3] << 16);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (p4 + k >= lo && p4 + k < hi) {
+          s->prev[ridx(p4 + k)] = (uint16_t)hk[k];
+          s->link4[(p4 + k) & (DF_SUB - 1)] = (uint16_t)h4[k];
+        }
+      }
+    }
+  }
+#endif
 }
 
 #ifndef ZT_CL_U
@@ -1970,21 +2005,39 @@ __global__ __launch_bounds__(64) void block_kernel(DeflateParams P) {
 }
 
 // ================================ 3. encode_kernel ================================
+#ifndef ZT_ENC_LDS
+#define ZT_ENC_LDS 1  // block words staged in LDS, then written out coalesced
+#endif
+#ifndef ZT_ENC_CACHE
+#define ZT_ENC_CACHE (ZT_DF_GROUP == 1)  // a thread's first tokens kept in registers between the two passes
+#endif
+constexpr int ENC_CACHE = 16;
+// a dynamic block is never planned larger than its stored form
+// (block_kernel); a fixed-code block (compressionType FIXED) may take 9 bits
+// per byte: 36 KiB + header and marker
+constexpr uint32_t ENC_OBUF_WORDS = (ZT_ENC_LDS ? (DF_GROUP * DF_BLOCK / 8 * 9 + 64) / 4 + 64 : 1);
 struct EncShared {
   uint32_t lit_code[288];
   uint32_t dist_code[32];
   uint32_t start[ENC_THREADS + 1];  // exclusive prefix of per-thread bit counts
   uint32_t first_val[ENC_THREADS];  // contribution to the (partial) first word
   uint32_t wsum[ENC_THREADS / 64];
+  uint32_t obuf[ENC_OBUF_WORDS];    // the block's words (ZT_ENC_LDS)
 };
 
 // a block's words in the stream: dst = the aligned word holding its first
 // byte; words 0 and `wlast` are shared with the neighbouring blocks (or the
-// restart marker), so only the block's own bytes [lo, hi) of them are stored
+// restart marker), so only the block's own bytes [lo, hi) of them are stored.
+// ZT_ENC_LDS: every word goes to the LDS buffer first -- each thread packs its
+// own few words, so direct stores left most lines of the stream partially
+// written per instruction (encode_kernel wrote 1.47 GB per GiB for 0.57 GB of
+// stream, profiles/r04k_pmc_traffic.txt) -- and flush() writes them out
+// coalesced.
 struct BlockWords {
   uint8_t *dst;
   uint32_t wlast, lo, hi;
-  __device__ __forceinline__ void store(uint32_t w, uint32_t v) const {
+  uint32_t *obuf;
+  __device__ __forceinline__ void store_global(uint32_t w, uint32_t v) const {
     if (w != 0 && w != wlast) {
       reinterpret_cast<uint32_t *>(dst)[w] = v;
       return;
@@ -1994,6 +2047,17 @@ struct BlockWords {
       const uint32_t x = 4 * w + b;
       if (x >= lo && x < hi) dst[x] = (uint8_t)(v >> (8 * b));
     }
+  }
+  __device__ __forceinline__ void store(uint32_t w, uint32_t v) const {
+    if (ZT_ENC_LDS)
+      obuf[w] = v;
+    else
+      store_global(w, v);
+  }
+  // after a workgroup barrier: words [0, wlast] from the LDS buffer
+  __device__ __forceinline__ void flush(uint32_t t) const {
+    if (!ZT_ENC_LDS) return;
+    for (uint32_t w = t; w <= wlast; w += ENC_THREADS) store_global(w, obuf[w]);
   }
 };
 
@@ -2181,10 +2245,39 @@ __global__ __launch_bounds__(ENC_THREADS) void encode_kernel(DeflateParams P) {
   const uint32_t b = (uint32_t)(((uint64_t)ntok * (t + 1)) / ENC_THREADS);
   uint32_t bits = 0;
   const uint32_t *tok = P.res + (uint64_t)blk * DF_BLOCK;  // (DF_GROUP 1: the block's own tokens)
+#if ZT_ENC_CACHE
+  // the thread's first ENC_CACHE tokens stay in registers for the packing
+  // pass (5 aligned 16-byte loads, then a shift by a % 4): only the rest is
+  // read twice
+  typedef unsigned int u32x4e __attribute__((ext_vector_type(4)));
+  const uint32_t nc = b - a < (uint32_t)ENC_CACHE ? b - a : (uint32_t)ENC_CACHE;
+  uint32_t cache[ENC_CACHE];
+  {
+    uint32_t raw[ENC_CACHE + 4];
+    const u32x4e *v = reinterpret_cast<const u32x4e *>(tok + (a & ~3u));
+#pragma unroll
+    for (int q = 0; q < ENC_CACHE / 4 + 1; ++q) {
+      const u32x4e x = (4 * q < (int)((a & 3) + nc)) ? v[q] : u32x4e{0, 0, 0, 0};
+      raw[4 * q] = x.x;
+      raw[4 * q + 1] = x.y;
+      raw[4 * q + 2] = x.z;
+      raw[4 * q + 3] = x.w;
+    }
+    const uint32_t sh = a & 3;
+#pragma unroll
+    for (int j = 0; j < ENC_CACHE; ++j)
+      cache[j] = sh == 0 ? raw[j] : sh == 1 ? raw[j + 1] : sh == 2 ? raw[j + 2] : raw[j + 3];
+  }
+#pragma unroll
+  for (int j = 0; j < ENC_CACHE; ++j)
+    if ((uint32_t)j < nc) bits += token_bits(s, cache[j]);
+  for_tokens(tok, a + nc, b, [&](uint32_t tk) { bits += token_bits(s, tk); });
+#else
   if constexpr (DF_GROUP == 1)
     for_tokens(tok, a, b, [&](uint32_t tk) { bits += token_bits(s, tk); });
   else
     for_group_tokens(P, plan, blk, a, b, [&](uint32_t tk) { bits += token_bits(s, tk); });
+#endif
   if (t == 0) bits += hdr_bits;
   const uint32_t eob = s->lit_code[256] >> 16;
   if (t == ENC_THREADS - 1) bits += eob;  // marker bits appended after the scan
@@ -2218,6 +2311,11 @@ __global__ __launch_bounds__(ENC_THREADS) void encode_kernel(DeflateParams P) {
   bw.lo = B0 >> 3;
   bw.hi = (B0 + block_end) >> 3;
   bw.wlast = (B0 + block_end - 1) >> 5;
+  bw.obuf = s->obuf;
+  if (ZT_ENC_LDS && bw.wlast >= ENC_OBUF_WORDS) {  // (cannot happen: see ENC_OBUF_WORDS)
+    if (t == 0) atomicOr(P.fault, 1u);
+    return;
+  }
   BitOut bo;
   // thread 0 starts at the header: its complete words come from the slot
   // (block_kernel), then its partial last word
@@ -2228,10 +2326,17 @@ __global__ __launch_bounds__(ENC_THREADS) void encode_kernel(DeflateParams P) {
     for (uint32_t k = 0; k < (hdr_bits >> 5); ++k) bo.put(hw[k], 32);
     if (hdr_bits & 31) bo.put(plan->hdr_tail, hdr_bits & 31);
   }
+#if ZT_ENC_CACHE
+#pragma unroll
+  for (int j = 0; j < ENC_CACHE; ++j)
+    if ((uint32_t)j < nc) put_token(bo, s, cache[j]);
+  for_tokens(tok, a + nc, b, [&](uint32_t tk) { put_token(bo, s, tk); });
+#else
   if constexpr (DF_GROUP == 1)
     for_tokens(tok, a, b, [&](uint32_t tk) { put_token(bo, s, tk); });
   else
     for_group_tokens(P, plan, blk, a, b, [&](uint32_t tk) { put_token(bo, s, tk); });
+#endif
   if (t == ENC_THREADS - 1) {
     const uint32_t c = s->lit_code[256];
     bo.put(c & 0xFFFF, c >> 16);
@@ -2255,6 +2360,10 @@ __global__ __launch_bounds__(ENC_THREADS) void encode_kernel(DeflateParams P) {
       if (ue >= (w + 1) * 32) break;
     }
     bw.store(w, v);
+  }
+  if (ZT_ENC_LDS) {
+    __syncthreads();
+    bw.flush(t);
   }
 }
 
