@@ -1465,7 +1465,7 @@ __device__ uint32_t parse_block(S *s, ParseStage *st, const DeflateParams &P, ui
 // price_kernel: the greedy parse of the block gives symbol statistics; their
 // entropy gives a price per literal, length and distance symbol (1/8 bit
 // units, <= 15 bits per symbol).  optparse_kernel:  Each lane then runs a backward shortest-path DP over its own
-// 512-position segment (plus 128 positions of the next segment, where paths
+// 512-position segment (plus OP_OV = 64 positions of the next segment, where paths
 // have converged): C[i] = min(lit(i) + C[i+1], min_l len(l) + dist(D_i) +
 // C[i+l]) over l in 3..min(L_i, 16) and l = L_i, for the longest match
 // (L_i, D_i) the match kernel found at i.  The chosen length is written over
@@ -1477,7 +1477,10 @@ __device__ uint32_t parse_block(S *s, ParseStage *st, const DeflateParams &P, ui
 // distinct banks): differences over <= 258 positions stay below 2^15.
 typedef unsigned int op_u32x4 __attribute__((ext_vector_type(4)));
 constexpr int OP_SEG = DF_BLOCK / 64;  // one segment per lane
-constexpr int OP_OV = 128;
+#ifndef ZT_OP_OV
+#define ZT_OP_OV 64  // 128 / 96 / 64 / 32: post-match 7.64 / 7.50 / 7.42 / 7.28 ms per GiB, worst ratio window 1.0179 / 1.0180 / 1.0182 / 1.0195 (tools/gpu_r04ov.sh)
+#endif
+constexpr int OP_OV = ZT_OP_OV;  // positions of the next segment each lane's DP runs over (paths converge)
 // C ring rows: C[i + l] for l <= OP_RING.  A longer match reads C[i + OP_RING]
 // instead of C[i + L] (an estimate of its continuation: the parse stays
 // valid, only the DP's cost model is approximate there); 64 rows and 3
