@@ -124,6 +124,8 @@ struct DeflateParams {
   uint64_t halo;
   uint64_t end;         // halo + n
   uint32_t blocks_per_wg;
+  uint32_t big_wgs;     // match workgroups [0, big_wgs) take blocks_per_wg blocks, later ones tail_k
+  uint32_t tail_k;
   uint32_t nblocks;
   uint32_t restart;     // blocks per independent segment (multiple of blocks_per_wg)
   uint32_t hist_max;    // history bytes a super-chunk loads (multiple of DF_SUB, <= DF_HIST)
@@ -855,8 +857,10 @@ __global__ __launch_bounds__(DF_THREADS) void match_kernel(DeflateParams P) {
   // that every XCD gets its share of those
   uint32_t wg = blockIdx.x;
   if ((wg | 7u) < gridDim.x) wg = (wg & ~7u) | ((wg + (wg >> 3)) & 7u);
-  const uint32_t b0 = wg * P.blocks_per_wg;
-  const uint32_t b1 = (b0 + P.blocks_per_wg) < P.nblocks ? (b0 + P.blocks_per_wg) : P.nblocks;
+  const bool big = wg < P.big_wgs;
+  const uint32_t b0 = big ? wg * P.blocks_per_wg : P.big_wgs * P.blocks_per_wg + (wg - P.big_wgs) * P.tail_k;
+  const uint32_t kb = big ? P.blocks_per_wg : P.tail_k;
+  const uint32_t b1 = (b0 + kb) < P.nblocks ? (b0 + kb) : P.nblocks;
   if (P.store) {  // every block of the super-chunk goes stored: nothing to search
     bool all = true;
     for (uint32_t b = b0; b < b1; ++b) all = all && P.store[b];
@@ -2474,7 +2478,7 @@ static DeflateLevel level_params(int level) {
 // 8 / 4 / 2 blocks 31.8 / 30.7 / 31.4 ms), a power of two so segments (32
 // blocks) align.
 struct DeflateGeom {
-  uint32_t nblocks, k, nwg;
+  uint32_t nblocks, k, nwg, big_wgs, tail_k;
   size_t res_bytes, slot_bytes, len_bytes, off_bytes, plan_bytes, store_bytes;
 };
 
@@ -2489,6 +2493,25 @@ static size_t deflate_geometry(const DeviceCtx *c, size_t n, DeflateGeom *g) {
   while (k2 < kk && k2 < cap) k2 <<= 1;
   g->k = k2;
   g->nwg = (g->nblocks + k2 - 1) / k2;
+  // the last round of workgroups is the tail where CUs run dry: its blocks go
+  // to one-block workgroups (streams identical; 1 GiB bench, match kernel
+  // 25.47 -> 24.85 ms; 2-block tail 25.03, two tail rounds 24.92, 8-block
+  // workgroups + tail 25.5: tools/gpu_r04tail*.sh).  Tuning hooks:
+  // ZT_DF_TAILK = blocks per tail workgroup (0 = none), ZT_DF_TAILR = tail
+  // rounds of num_cu workgroups
+  static const int tk_env = getenv("ZT_DF_TAILK") ? atoi(getenv("ZT_DF_TAILK")) : -1;
+  static const int tr_env = getenv("ZT_DF_TAILR") ? atoi(getenv("ZT_DF_TAILR")) : 1;
+  const uint32_t tk = tk_env >= 0 ? (uint32_t)tk_env : 1u;
+  g->big_wgs = g->nwg;
+  g->tail_k = k2;
+  if (tk > 0 && tk < k2 && (k2 % tk) == 0 && tr_env > 0) {
+    const uint64_t tail = (uint64_t)tr_env * c->num_cu * k2;
+    if ((uint64_t)g->nblocks > tail) {
+      g->big_wgs = (uint32_t)((g->nblocks - tail) / k2);
+      g->tail_k = tk;
+      g->nwg = g->big_wgs + (g->nblocks - g->big_wgs * k2 + tk - 1) / tk;
+    }
+  }
   g->res_bytes = ((size_t)g->nblocks * DF_BLOCK * 4 + 255) & ~size_t(255);
   g->slot_bytes = (size_t)g->nblocks * DF_SLOT;
   g->len_bytes = ((size_t)g->nblocks * 4 + 255) & ~size_t(255);
@@ -2553,6 +2576,8 @@ int deflate_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t halo, in
   P.halo = halo;
   P.end = halo + n;
   P.blocks_per_wg = G.k;
+  P.big_wgs = G.big_wgs;
+  P.tail_k = G.tail_k;
   P.nblocks = G.nblocks;
   P.restart = (restart_blocks() + G.k - 1) / G.k * G.k;
   // tuning hook: ZT_DF_HIST = KiB of history per super-chunk (multiple of 4, <= 28)
@@ -2663,6 +2688,8 @@ int deflate_batch_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t count, const
   P.halo = 0;
   P.end = padded;
   P.blocks_per_wg = 1;
+  P.big_wgs = G.nblocks;
+  P.tail_k = 1;
   P.nblocks = G.nblocks;
   P.restart = restart_blocks();
   P.hist_max = DF_HIST;
