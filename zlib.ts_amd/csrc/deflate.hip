@@ -1497,7 +1497,7 @@ constexpr int OP_OV = ZT_OP_OV;  // positions of the next segment each lane's DP
 #endif
 constexpr int OP_RING = ZT_OP_RING;
 #ifndef ZT_OP_SHORT
-#define ZT_OP_SHORT 20  // 8..14 / 16 / 18 / 20: worst ratio window 1.042..1.026 / 1.0182 / 1.0153 / 1.0144 at chain 28, the headroom spent on level 6's chain 28 -> 22 (tools/gpu_r04os*.sh)
+#define ZT_OP_SHORT 24  // 8..14 / 16 / 18 / 20: worst ratio window 1.042..1.026 / 1.0182 / 1.0153 / 1.0144 at chain 28; at chain 20: 20 / 24 / 28 1.0207 / 1.0190 / 1.0188 -- the headroom spent on level 6's chain 28 -> 20 (profiles/r04os_sweep.txt)
 #endif
 constexpr int OP_SHORT = ZT_OP_SHORT;  // every cut length 3..OP_SHORT is tried (even), longer ones only at L
 static_assert(OP_SHORT % 2 == 0 && OP_SHORT >= 4, "cut lengths go in pairs");
@@ -1586,7 +1586,7 @@ __device__ __forceinline__ uint32_t op_min3(uint32_t a, uint32_t b, uint32_t c) 
 }
 
 #ifndef ZT_OP_MINW
-#define ZT_OP_MINW 3  // waves per SIMD the register budget must allow (168 VGPRs: cut lengths to 20 take 134; at 4 waves, 128 VGPRs, they spill: optparse +0.1 ms)
+#define ZT_OP_MINW 3  // waves per SIMD the register budget must allow (168 VGPRs: cut lengths to 24 take 138; at 4 waves, 128 VGPRs, 20 and more spill: optparse +0.1 ms)
 #endif
 __global__ __launch_bounds__(64, ZT_OP_MINW) void optparse_kernel(DeflateParams P) {
   __shared__ OptShared sh;
@@ -2471,10 +2471,10 @@ static DeflateLevel level_params(int level) {
     case 9: return {512, 258, 1, 4096, 258, 8, 16, 258, 1};
     // 6: chain 28 since matches run past 4 KiB sub-chunk ends (DF_HEAD): the
     // 16-window gate's wordsalad worst 1.0179 (chain 32 without heads:
-    // 1.0171), 5 % less chain walking (profiles/r04j_gate.log); 22 since the
-    // DP tries cut lengths up to 20 (OP_SHORT): worst window 1.0185, match
-    // 24.9 -> 23.1 ms per GiB (profiles/r04os_sweep.txt)
-    default: return {22, 128, 1, 4096, 128, 8, 16, 16, 1};  // 6
+    // 1.0171), 5 % less chain walking (profiles/r04j_gate.log); 20 since the
+    // DP tries cut lengths up to 24 (OP_SHORT): worst window 1.0190, match
+    // 24.9 -> 22.4 ms per GiB (chain 18: 1.0225; profiles/r04os_sweep.txt)
+    default: return {20, 128, 1, 4096, 128, 8, 16, 16, 1};  // 6
   }
 }
 
