@@ -1468,10 +1468,11 @@ __device__ uint32_t parse_block(S *s, ParseStage *st, const DeflateParams &P, ui
 // Cost-based parse of one 32 KiB block per wavefront (levels with opt = 1).
 // price_kernel: the greedy parse of the block gives symbol statistics; their
 // entropy gives a price per literal, length and distance symbol (1/8 bit
-// units, <= 15 bits per symbol).  optparse_kernel:  Each lane then runs a backward shortest-path DP over its own
-// 512-position segment (plus OP_OV = 64 positions of the next segment, where paths
-// have converged): C[i] = min(lit(i) + C[i+1], min_l len(l) + dist(D_i) +
-// C[i+l]) over l in 3..min(L_i, 16) and l = L_i, for the longest match
+// units, <= 15 bits per symbol).  optparse_kernel: each lane runs a backward
+// shortest-path DP over its own 512-position segment (plus OP_OV = 64
+// positions of the next segment, where paths have converged): C[i] =
+// min(lit(i) + C[i+1], min_l len(l) + dist(D_i) + C[i+l]) over l in
+// 3..min(L_i, OP_SHORT) and l = L_i, for the longest match
 // (L_i, D_i) the match kernel found at i.  The chosen length is written over
 // res[i] (0 = literal), so the block kernel's parse follows the DP's path.
 // Every value left in res is a valid (shorter or equal) match, so the stream
@@ -1487,11 +1488,11 @@ constexpr int OP_SEG = DF_BLOCK / 64;  // one segment per lane
 constexpr int OP_OV = ZT_OP_OV;  // positions of the next segment each lane's DP runs over (paths converge)
 // C ring rows: C[i + l] for l <= OP_RING.  A longer match reads C[i + OP_RING]
 // instead of C[i + L] (an estimate of its continuation: the parse stays
-// valid, only the DP's cost model is approximate there); 64 rows and 3
-// prefetched groups keep the LDS at 8.5 KiB and the VGPRs at 126 per wave (4
-// waves per SIMD; 80 rows / 4 groups: 3, 2.83 -> 2.73 ms per GiB,
-// profiles/r02q_optparse_variants.txt); bench ratio unchanged to 5 digits
-// (260 rows: 1 wave per SIMD)
+// valid, only the DP's cost model is approximate there); 64 rows keep the
+// LDS at 8.5 KiB (round 2, 16-position groups: 80 rows / 4 groups, 3 waves
+// per SIMD, 2.83 ms against 2.73 at 64 / 3 and 4 waves,
+// profiles/r02q_optparse_variants.txt; bench ratio unchanged to 5 digits;
+// 260 rows: 1 wave per SIMD)
 #ifndef ZT_OP_RING
 #define ZT_OP_RING 64
 #endif
@@ -2481,7 +2482,8 @@ static DeflateLevel level_params(int level) {
 // Work split: enough workgroups to cover every CU twice, at most 4 blocks
 // (128 KiB) per workgroup (small super-chunks balance uneven data across
 // CUs; each loads 28 KiB of history; 1 GiB mixed corpus, match kernel:
-// 8 / 4 / 2 blocks 31.8 / 30.7 / 31.4 ms), a power of two so segments (32
+// 8 / 4 / 2 blocks 31.8 / 30.7 / 31.4 ms in round 2; round 4: 26.65 / 25.44 /
+// 25.75 ms, 16 blocks 29.6, tools/gpu_r04sup.sh), a power of two so segments (32
 // blocks) align.
 struct DeflateGeom {
   uint32_t nblocks, k, nwg, big_wgs, tail_k;
