@@ -2023,7 +2023,10 @@ __global__ __launch_bounds__(64) void block_kernel(DeflateParams P) {
 #ifndef ZT_ENC_CACHE
 #define ZT_ENC_CACHE (ZT_DF_GROUP == 1)  // a thread's first tokens kept in registers between the two passes
 #endif
-constexpr int ENC_CACHE = 16;
+#ifndef ZT_ENC_NCACHE
+#define ZT_ENC_NCACHE 32  // 16 / 32 / 48 / 64: encode 1.19 / 1.10 / 1.16 / 1.55 ms per GiB; L2 read requests 1.96 -> 1.16 GB (the second pass's re-reads missed L2; tools/gpu_r04ec*.sh)
+#endif
+constexpr int ENC_CACHE = ZT_ENC_NCACHE;  // tokens per thread kept (a multiple of 4)
 // a dynamic block is never planned larger than its stored form
 // (block_kernel); a fixed-code block (compressionType FIXED) may take 9 bits
 // per byte: 36 KiB + header and marker
