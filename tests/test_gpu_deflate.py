@@ -345,3 +345,37 @@ def test_device_chain_falls_back(zt, oracle):
         _plan_inflate(zt, s3, len(d3) - 1)
     olen, eip, out = _plan_inflate(zt, s3, len(d3))
     assert olen == len(d3) and out[:olen] == d3
+
+
+def test_tail_split_streams_identical(zt, oracle):
+    """The match kernel's last round of workgroups takes one block each
+    (deflate_geometry: ZT_DF_TAILK) instead of the super-chunk's four: every
+    position is linked and searched alike whatever workgroup holds it, so the
+    stream of an input large enough to have a tail round (48 MiB: 1536 blocks,
+    1024 of them in one-block workgroups on 256 CUs) is byte-identical to the
+    one without the split (a child process with ZT_DF_TAILK=0), and decodes."""
+    import hashlib
+    import json
+    import os
+    import subprocess
+    import sys
+
+    import torch
+
+    n = 48 << 20
+    d_in = torch.empty(n, dtype=torch.uint8, device="cuda")
+    d_c = torch.empty(zt.deflate_bound(n), dtype=torch.uint8, device="cuda")
+    zt.synth_dev("mixed", 7, d_in.data_ptr(), n)
+    dp = zt.DeflatePlan(n, level=6)
+    clen = dp.run(d_in.data_ptr(), n, d_c.data_ptr())
+    dp.close()
+    torch.cuda.synchronize()
+    s = d_c[:clen].cpu().numpy().tobytes()
+    assert zlib.decompress(s, -15) == d_in.cpu().numpy().tobytes()
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, ZT_DF_TAILK="0")
+    p = subprocess.run([sys.executable, os.path.join(here, "tail_split_child.py")], env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    child = json.loads(p.stdout.strip().splitlines()[-1])
+    assert child == {"len": clen, "sha256": hashlib.sha256(s).hexdigest()}
