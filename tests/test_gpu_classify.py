@@ -86,3 +86,33 @@ def test_classify_batch_and_fixed(zt, oracle):
     assert zt.timing_read()["blocks_unsearched"] == 0
     zt.timing_enable(False)
     assert zlib.decompress(s, -15) == files[0]
+
+
+def test_classify_entropy_band(zt):
+    # 240 equiprobable byte values: ~7.91 bits per byte, above the 4 KiB
+    # sample's 7.85 cut but ~1 % below 8: the whole-block entropy (stage C)
+    # must send every block to the search / Huffman coding, not store it
+    rng = random.Random(11)
+    d = bytes(rng.randrange(240) for _ in range(256 << 10))
+    s, n = _deflate_count(zt, d)
+    assert n == 0
+    assert zlib.decompress(s, -15) == d
+    assert len(s) < len(d) * 0.995
+
+
+def test_classify_random_sample_over_filler(zt):
+    # random bytes exactly where stage A samples (1 KiB at each quarter of a
+    # block) over 4-bit filler without 8-byte repeats: the sample looks
+    # incompressible, the block is not (stage C counts all of it)
+    rng = random.Random(12)
+    blocks = []
+    for _ in range(4):
+        blk = bytearray(rng.getrandbits(4) * 17 for _ in range(32768))
+        for q in range(4):
+            blk[q * 8192:q * 8192 + 1024] = bytes(rng.getrandbits(8) for _ in range(1024))
+        blocks.append(bytes(blk))
+    d = b"".join(blocks)
+    s, n = _deflate_count(zt, d)
+    assert n == 0
+    assert zlib.decompress(s, -15) == d
+    assert len(s) < len(d) * 0.75

@@ -14,7 +14,9 @@
 // new Deflate(input).compress() (src/Deflate.ts:60-99) and
 // new RawDeflate(input).compress() (src/RawDeflate.ts:87-114).
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -29,6 +31,31 @@ namespace zt {
 namespace {
 
 constexpr uint64_t kBlk = 32768;
+
+// ZT_BATCH_STAGES=1: host-only stage timers of one device's share (JSON line
+// on stderr per share) -- packing into pinned staging and framing the members
+// are the host work that has to keep up with k devices on a node
+// (tools/c4_host_stages.py).  Measurement only.
+double stage_now() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+bool stages_on() {
+  static const bool on = getenv("ZT_BATCH_STAGES") != nullptr;
+  return on;
+}
+struct StageTimes {
+  double pack_ms = 0, frame_ms = 0, wall_ms = 0;
+  uint64_t in_bytes = 0, out_bytes = 0;
+  size_t items = 0, groups = 0;
+  void report(int dev) const {
+    if (!stages_on()) return;
+    fprintf(stderr,
+            "{\"zt_batch_stages\": 1, \"device\": %d, \"items\": %zu, \"groups\": %zu, \"in_bytes\": %llu, "
+            "\"out_bytes\": %llu, \"pack_ms\": %.3f, \"frame_ms\": %.3f, \"wall_ms\": %.3f}\n",
+            dev, items, groups, (unsigned long long)in_bytes, (unsigned long long)out_bytes, pack_ms, frame_ms,
+            wall_ms);
+  }
+};
 
 size_t round_blk(size_t n) { return (n + kBlk - 1) / kBlk * kBlk; }
 
@@ -83,7 +110,7 @@ constexpr uint64_t kGroupMin = 256ull << 20;
 
 int batch_grouped(DeviceCtx *c, const uint8_t *const *in, const std::vector<size_t> &work,
                   const std::vector<uint64_t> &off, const std::vector<uint64_t> &len, uint64_t padded, int ct, int lv,
-                  const Framing &fr, uint8_t **out, size_t *out_len) {
+                  const Framing &fr, uint8_t **out, size_t *out_len, StageTimes &tm) {
   const size_t m = work.size();
   const bool sums = fr.kind != Framing::RAW;
   // groups [gk[g], gk[g + 1]) of items
@@ -165,11 +192,13 @@ int batch_grouped(DeviceCtx *c, const uint8_t *const *in, const std::vector<size
       uint8_t *st = stage_in[g & 1];
       if (g >= 2) ZT_HIP(hipEventSynchronize(staged[g & 1]));  // its previous upload has left
       const uint64_t b = gbeg(g), nb = gk[g + 1] - gk[g];
+      const double t0 = stage_now();
       parallel_copy(nb, [&](size_t j) {
         const size_t k = gk[g] + j;
         memcpy(st + off[k] - b, in[work[k]], len[k]);
         memset(st + off[k] - b + len[k], 0, round_blk(len[k]) - len[k]);
       }, gend(g) - b);
+      tm.pack_ms += stage_now() - t0;  // (this thread only)
       ZT_HIP(hipMemcpyAsync((uint8_t *)d_in + b, st, gend(g) - b, hipMemcpyHostToDevice, c->up));
       ZT_HIP(hipEventRecord(staged[g & 1], c->up));
       ZT_HIP(hipEventRecord(landed[g], c->up));
@@ -190,6 +219,7 @@ int batch_grouped(DeviceCtx *c, const uint8_t *const *in, const std::vector<size
       ZT_HIP(hipStreamSynchronize(c->dn));
       std::vector<int> rcs(nb, ZT_OK);
       std::vector<size_t> soff;
+      const double t0 = stage_now();
       uint8_t *slab = frame_slab(fr, go, nb, soff);
       if (!slab) return set_error(ZT_E_NOMEM, "host allocation failed");
       parallel_copy(nb, [&](size_t j) {
@@ -197,6 +227,8 @@ int batch_grouped(DeviceCtx *c, const uint8_t *const *in, const std::vector<size
         rcs[j] = frame_item(fr, len[k], stage_out + go[j], go[j + 1] - go[j], hsums[2 * k], hsums[2 * k + 1], &out[i],
                             &out_len[i], slab + soff[j]);
       }, go[nb]);
+      tm.frame_ms += stage_now() - t0;  // (this thread only)
+      tm.out_bytes += go[nb];
       for (int rc : rcs)
         if (rc) return rc;
     }
@@ -238,6 +270,7 @@ int batch_grouped(DeviceCtx *c, const uint8_t *const *in, const std::vector<size
   }
   tu.join();
   td.join();
+  tm.groups = ng;
   if (err) return set_error(err, err_msg);
   return ZT_OK;
 }
@@ -276,18 +309,34 @@ int batch_on_device(int dev, const uint8_t *const *in, const size_t *n, const st
     padded += round_blk(len[k]);
     in_bytes += len[k];
   }
+  StageTimes tm;
+  tm.items = m;
+  tm.in_bytes = in_bytes;
+  const double t_start = stage_now();
+  struct Report {
+    StageTimes &tm;
+    double t0;
+    int dev;
+    ~Report() {
+      tm.wall_ms = stage_now() - t0;
+      tm.report(dev);
+    }
+  } report{tm, t_start, dev};
   if (ct != 0 && padded >= kGroupMin && m >= 2) {
-    const int rc = batch_grouped(c, in, work, off, len, padded, ct, lv, fr, out, out_len);
+    const int rc = batch_grouped(c, in, work, off, len, padded, ct, lv, fr, out, out_len, tm);
     return rc ? fail(rc) : ZT_OK;
   }
   void *d_in, *h_stage;
   if (int rc = scratch(c, 0, padded + 64, &d_in)) return fail(rc);
   if (int rc = pinned(c, padded, &h_stage, 0)) return fail(rc);
   uint8_t *stage = static_cast<uint8_t *>(h_stage);
+  const double t_pack = stage_now();
   parallel_copy(m, [&](size_t k) {
     memcpy(stage + off[k], in[work[k]], len[k]);
     memset(stage + off[k] + len[k], 0, round_blk(len[k]) - len[k]);
   }, in_bytes);
+  tm.pack_ms += stage_now() - t_pack;
+  tm.groups = 1;
   ZT_HIP(hipMemcpyAsync(d_in, stage, padded, hipMemcpyHostToDevice, c->stream));
   // checksums on the second stream, over the same device bytes
   std::vector<uint32_t> hsums(2 * m, 0);
@@ -351,6 +400,7 @@ int batch_on_device(int dev, const uint8_t *const *in, const size_t *n, const st
   int first_rc = ZT_OK;
   std::vector<int> rcs(m, ZT_OK);
   std::vector<size_t> soff;
+  const double t_frame = stage_now();
   uint8_t *slab = frame_slab(fr, oo.data(), m, soff);
   if (!slab) return fail(set_error(ZT_E_NOMEM, "host allocation failed"));
   parallel_copy(m, [&](size_t k) {
@@ -358,6 +408,8 @@ int batch_on_device(int dev, const uint8_t *const *in, const size_t *n, const st
     rcs[k] = frame_item(fr, len[k], body_host + oo[k], oo[k + 1] - oo[k], hsums[2 * k], hsums[2 * k + 1], &out[i],
                         &out_len[i], slab + soff[k]);
   }, oo[m]);
+  tm.frame_ms += stage_now() - t_frame;
+  tm.out_bytes += oo[m];
   for (int rc : rcs)
     if (rc && !first_rc) first_rc = rc;
   return first_rc ? fail(first_rc) : ZT_OK;

@@ -268,7 +268,11 @@ __device__ inline uint32_t shift_bytes(const uint32_t *__restrict__ dig, const u
 // segments' (already end-shifted) results to `acc` by atomics, workgroup 0
 // adds the caller's initial CRC shifted over the whole buffer, and the
 // workgroup that arrives last writes the final values and leaves `acc`
-// zeroed for the next call (calls on a context are serialised by its mutex).
+// zeroed for the next call.  One accumulator per device context: correctness
+// rests on every caller of checksums_dev synchronising the launch stream
+// before it releases the context mutex (zt_dev_checksums waits on its stream,
+// the container calls on c->aux through AuxWait), so no two launches share
+// `acc` at once; an asynchronous caller would need its own accumulator.
 // A separate one-workgroup finish kernel cost 6 us + its launch per call.
 struct CkFinish {
   CkAcc *acc;  // null: batch mode (per-segment results to `out`)

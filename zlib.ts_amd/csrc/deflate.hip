@@ -84,7 +84,11 @@ static_assert(DF_SLOT >= 321 * 4 && DF_SLOT * 8 >= 17 + 19 * 3 + 316 * 14, "slot
 // table (u32 heads, no chains): the sizes fill the 160 KiB of LDS next to the
 // ring, the chain links and the sub-chunk's 4-byte links
 #ifndef ZT_DF_HSIZE
+#ifdef ZT_DF_HEAD16
+#define ZT_DF_HSIZE 24528  // (u16 heads, two per word)
+#else
 #define ZT_DF_HSIZE 12240
+#endif
 #endif
 #ifndef ZT_DF_H4SIZE
 #define ZT_DF_H4SIZE 2048
@@ -243,11 +247,16 @@ __device__ __forceinline__ uint32_t res_byte(uint32_t r) { return r >> 24; }
 //     from registers (each thread 128 consecutive positions); a repeat of L
 //     bytes gives ~L / 16 hits (the pair's other position, before or after,
 //     within a match distance).  CL_HITS hits or more -> search.
+//  C. the whole block's byte histogram (counted from the registers stage B
+//     loaded): a block whose order-0 entropy would let an ideal literal coder
+//     save more than CL_SAVE over the stored form is searched (a skewed
+//     block -- 7.85..7.98 bits -- or compressible bytes outside the sample).
 // Everything else is flagged: match / price / DP / parse skip the block and
 // block_kernel plans it stored (the smallest form for such bytes: the
 // reference's dynamic block of random data is 0.1 % larger).
 constexpr float CL_ENTROPY = 7.85f;  // uniform bytes: ~7.955 from a 4096-byte sample
 constexpr uint32_t CL_HITS = 8;
+constexpr float CL_SAVE = 0.002f;  // C: largest saving an ideal literal coder may forgo
 constexpr uint32_t CL_TABLE = 8192;
 constexpr uint32_t CL_EMPTY = 0xFFFFFFFFu;
 struct ClassifyShared {
@@ -329,6 +338,7 @@ __global__ __launch_bounds__(256) void classify_kernel(DeflateParams P) {
   if (h0 < floor_) h0 = floor_;
   const uint32_t wlen = (uint32_t)((int64_t)lo + blen - h0);
   for (uint32_t i = t; i < CL_TABLE; i += 256) s->table[i] = CL_EMPTY;
+  s->hist[t] = 0;  // (stage A's reads of it are behind the barrier above; B2 counts the whole block)
   // B1. inserts: every 16th position of the window (at most 15 per thread,
   // every load issued before the first is used); 8-byte loads when the
   // stream is 16-byte aligned and the window's reads stay inside it
@@ -387,6 +397,10 @@ __global__ __launch_bounds__(256) void classify_kernel(DeflateParams P) {
 #pragma unroll
       for (int j = 0; j < 34; ++j) w[j] = cl_gword(g, (int64_t)(lo + k0 + 4 * j), n);
     }
+    // the whole block's byte histogram (stage A saw a 4 KiB sample only)
+#pragma unroll
+    for (int k = 0; k < 128; ++k)
+      if (k0 + (uint32_t)k < blen) atomicAdd(&s->hist[(w[k >> 2] >> (8 * (k & 3))) & 0xFF], 1u);
 #pragma unroll
     for (int k = 0; k < 128; ++k) {
       const uint32_t x0 = (k & 3) ? __builtin_amdgcn_alignbyte(w[(k >> 2) + 1], w[k >> 2], k & 3) : w[k >> 2];
@@ -403,18 +417,35 @@ __global__ __launch_bounds__(256) void classify_kernel(DeflateParams P) {
   for (int off = 32; off; off >>= 1) hits += __shfl_xor(hits, off, 64);
   if ((t & 63) == 0) s->hits[t >> 6] = hits;
   __syncthreads();
+  // C. the whole block's order-0 entropy: an ideal literal coder (which no
+  // Huffman code beats) + a 32-byte header must not save more than
+  // CL_SAVE of the block over the stored form, or the block is searched
+  // (uniform bytes: ~7.994 bits per byte over 32 KiB, the cut ~7.98)
+  const float cb = (float)s->hist[t];
+  float eb = cb > 0.f ? cb * __log2f(cb) : 0.f;
+  for (int off = 32; off; off >>= 1) eb += __shfl_xor(eb, off, 64);
+  __syncthreads();  // (every hist read done before part[] is rewritten below)
+  if ((t & 63) == 0) s->part[t >> 6] = eb;
+  __syncthreads();
   if (t == 0) {
-    const bool st = (s->hits[0] + s->hits[1] + s->hits[2] + s->hits[3]) < CL_HITS;
+    const float hb = __log2f((float)blen) - (s->part[0] + s->part[1] + s->part[2] + s->part[3]) / (float)blen;
+    const bool flat = hb * (float)blen * 0.125f + 32.f >= (1.0f - CL_SAVE) * (float)blen;
+    const bool st = flat && (s->hits[0] + s->hits[1] + s->hits[2] + s->hits[3]) < CL_HITS;
     P.store[blk] = st ? 1 : 0;
     if (st) atomicAdd(P.nstore, 1u);
   }
 }
 
 // ================================ 1. match_kernel ================================
+constexpr uint32_t RING_ENT = DF_RING / 4;
 struct MatchShared {
   uint32_t ring[DF_RING / 4 + 16];  // data ring + 64-byte mirror of its start
   uint16_t prev[DF_RING];           // relative chain links (0 = none)
+#ifdef ZT_DF_HEAD16
+  uint32_t head[DF_HSIZE / 2];      // newest position (rel mod 2^16) per hash bucket, two buckets per word
+#else
   uint32_t head[DF_HSIZE];          // newest position (rel) per hash bucket
+#endif
   uint32_t head4[DF_H4SIZE];        // newest position (rel) per 4-byte-key bucket
   uint16_t link4[DF_SUB];           // position p of the sub-chunk: distance to the newest earlier
                                     // position of its 4-byte-key bucket (0 = none), at p % DF_SUB
@@ -431,15 +462,38 @@ struct MatchShared {
 __device__ __forceinline__ void lds_barrier() { __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 __device__ __forceinline__ uint32_t ridx(uint32_t rel) { return rel & (DF_RING - 1); }
-__device__ __forceinline__ uint32_t ld8(const MatchShared *s, uint32_t rel) {
-  return reinterpret_cast<const uint8_t *>(s->ring)[ridx(rel)];
+// ---- ring storage: every access goes through these ----
+// dword w (0 <= w < RING_ENT) of the ring := v (and its mirror copies)
+__device__ __forceinline__ void ring_put32(MatchShared *s, uint32_t w, uint32_t v) {
+  s->ring[w] = v;
+  if (w < 16) s->ring[RING_ENT + w] = v;
 }
-// 4 bytes at any byte offset: two aligned dwords and a byte align (an
+// byte k (0 <= k < DF_RING) of the ring := v (and its copies)
+__device__ __forceinline__ void ring_put8(MatchShared *s, uint32_t k, uint8_t v) {
+  uint8_t *rb = reinterpret_cast<uint8_t *>(s->ring);
+  rb[k] = v;
+  if (k < 64) rb[DF_RING + k] = v;
+}
+// dwords w and w + 1 of the ring (w < RING_ENT + 15: the mirror covers the wrap)
+__device__ __forceinline__ uint2 ring_pair(const MatchShared *s, uint32_t w) {
+  return make_uint2(s->ring[w], s->ring[w + 1]);
+}
+// dwords w .. w + N of the ring (w < RING_ENT, N <= 15: the mirror covers the wrap)
+template <int N>
+__device__ __forceinline__ void ring_dwords(const MatchShared *s, uint32_t w, uint32_t (&d)[N + 1]) {
+#pragma unroll
+  for (int k = 0; k <= N; ++k) d[k] = s->ring[w + k];
+}
+__device__ __forceinline__ uint32_t ld8(const MatchShared *s, uint32_t rel) {
+  const uint32_t i = ridx(rel);
+  return reinterpret_cast<const uint8_t *>(s->ring)[i];
+}
+// 4 bytes at any byte offset: an aligned dword pair and a byte align (an
 // unaligned ds_read_b32 is legal on gfx950 but measured 25-45 % slower here)
 __device__ __forceinline__ uint32_t ld32(const MatchShared *s, uint32_t rel) {
-  uint32_t i = ridx(rel);
-  uint32_t w = i >> 2;
-  return __builtin_amdgcn_alignbyte(s->ring[w + 1], s->ring[w], i & 3);
+  const uint32_t i = ridx(rel);
+  const uint2 v = ring_pair(s, i >> 2);
+  return __builtin_amdgcn_alignbyte(v.y, v.x, i & 3);
 }
 // chain key at p: the first klen bytes (kmask: bytes 0-3, kmask2: bytes 4-7)
 struct Key {
@@ -456,21 +510,13 @@ __device__ __forceinline__ uint32_t key4_hash(const MatchShared *s, uint32_t p) 
 
 // bytes [rel0, rel0 + len) of the super-chunk into the ring (len <= DF_SUB, rel0 % DF_SUB == 0)
 __device__ void load_sub(MatchShared *s, const uint8_t *g, uint32_t rel0, uint32_t len) {
-  uint8_t *rb = reinterpret_cast<uint8_t *>(s->ring);
   const uint32_t t = threadIdx.x;
   const uint32_t k0 = ridx(rel0);  // multiple of DF_SUB
   if (len == DF_SUB && (reinterpret_cast<uintptr_t>(g) & 3) == 0) {
-    const uint32_t v = reinterpret_cast<const uint32_t *>(g)[t];
-    s->ring[(k0 >> 2) + t] = v;
-    if (k0 == 0 && t < 16) s->ring[DF_RING / 4 + t] = v;
+    ring_put32(s, (k0 >> 2) + t, reinterpret_cast<const uint32_t *>(g)[t]);
     return;
   }
-  for (uint32_t i = t; i < len; i += DF_THREADS) {
-    uint8_t v = g[i];
-    uint32_t k = k0 + i;
-    rb[k] = v;
-    if (k < 64) rb[DF_RING + k] = v;
-  }
+  for (uint32_t i = t; i < len; i += DF_THREADS) ring_put8(s, k0 + i, g[i]);
 }
 
 // chain links for positions [lo, hi) (rel coords), by one wave, in position
@@ -504,7 +550,8 @@ __device__ __forceinline__ void hash_keys(MatchShared *s, uint32_t lo, uint32_t 
 #else
   for (uint32_t p4 = (lo & ~3u) + 4 * threadIdx.x; p4 < hi; p4 += 4 * DF_THREADS) {
     const uint32_t w = ridx(p4) >> 2;  // (the mirror past the ring's end holds w + 1, w + 2 at the wrap)
-    const uint32_t d0 = s->ring[w], d1 = s->ring[w + 1], d2 = s->ring[w + 2];
+    const uint2 d01 = ring_pair(s, w), d12 = ring_pair(s, w + 1);
+    const uint32_t d0 = d01.x, d1 = d01.y, d2 = d12.y;
     uint32_t hk[4], h4[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -554,11 +601,40 @@ __device__ void chain_link(MatchShared *s, uint32_t lo, uint32_t hi, Key key) {
     // branch-free: lanes past hi exchange with / link into a dummy word, so
     // the compiler keeps every load and exchange of the group in flight
     uint32_t old[CL_U];
+#ifdef ZT_DF_HEAD16
+    if (T == 0) {
+      // u16 heads: a masked-OR exchange of one half-word (ds_mskor_rtn_b32
+      // applies a wave's conflicting lanes in lane order, as the exchange
+      // does: tools/micro/lds_mskor_order.hip); the waits come after all CL_U
+      // are issued (the compiler does not see inline-asm LDS operations)
+      uint32_t sh[CL_U];
 #pragma unroll
-    for (int j = 0; j < CL_U; ++j) {
-      const uint32_t p = lo + (sb + j) * 64 + lane;
-      uint32_t *hp = p < hi ? (T == 0 ? &s->head[hq[j]] : &s->head4[hq[j]]) : &s->dummy[T];
-      old[j] = atomicExch(hp, p);
+      for (int j = 0; j < CL_U; ++j) {
+        const uint32_t p = lo + (sb + j) * 64 + lane;
+        uint32_t *hp = p < hi ? &s->head[hq[j] >> 1] : &s->dummy[T];
+        sh[j] = (hq[j] & 1) * 16;
+        const uint32_t a = (uint32_t)(uintptr_t)hp, clr = 0xFFFFu << sh[j], set = (p & 0xFFFFu) << sh[j];
+        __asm__ volatile("ds_mskor_rtn_b32 %0, %1, %2, %3" : "=v"(old[j]) : "v"(a), "v"(clr), "v"(set) : "memory");
+      }
+      static_assert(CL_U == 8, "the wait below names 8 results");
+      __asm__ volatile("s_waitcnt lgkmcnt(0)"
+                       : "+v"(old[0]), "+v"(old[1]), "+v"(old[2]), "+v"(old[3]), "+v"(old[4]), "+v"(old[5]),
+                         "+v"(old[6]), "+v"(old[7])::"memory");
+#pragma unroll
+      for (int j = 0; j < CL_U; ++j) {
+        const uint32_t p = lo + (sb + j) * 64 + lane;
+        // (the distance modulo 2^16 is exact: stale heads are re-aged by head_sweep)
+        old[j] = p - ((p - (old[j] >> sh[j])) & 0xFFFFu);
+      }
+    } else
+#endif
+    {
+#pragma unroll
+      for (int j = 0; j < CL_U; ++j) {
+        const uint32_t p = lo + (sb + j) * 64 + lane;
+        uint32_t *hp = p < hi ? (T == 0 ? &s->head[hq[j]] : &s->head4[hq[j]]) : &s->dummy[T];
+        old[j] = atomicExch(hp, p);
+      }
     }
     hashes(sb + CL_U, hq);
 #pragma unroll
@@ -575,6 +651,30 @@ __device__ void chain_link(MatchShared *s, uint32_t lo, uint32_t hi, Key key) {
                          __HIP_MEMORY_SCOPE_WORKGROUP);
   }
 }
+
+#ifdef ZT_DF_HEAD16
+// u16 heads hold rel positions modulo 2^16: every HEAD_SWEEP sub-chunks, at
+// rel position S (before that sub-chunk is linked), a head that is out of
+// reach (age > DF_MAXDIST, and not one of the <= DF_HEAD positions linked
+// ahead of S) is re-aged to S - 32768: until the next sweep it reads as
+// 32768..61440 back -- never a link -- and a head in reach stays below 2^16
+// back until then, so every link the exchange computes is the true distance.
+constexpr uint32_t HEAD_SWEEP = 4;
+static_assert(DF_MAXDIST + (HEAD_SWEEP + 1) * DF_SUB + DF_HEAD < 65536 - 1024, "ages stay below 2^16");
+__device__ __forceinline__ void head_sweep(MatchShared *s, uint32_t S) {
+  const uint32_t stale = (S - 32768u) & 0xFFFFu;
+  for (uint32_t i = threadIdx.x; i < DF_HSIZE / 2; i += DF_THREADS) {
+    const uint32_t w = s->head[i];
+    uint32_t r = w;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const uint32_t age = (S - (w >> (16 * k))) & 0xFFFFu;
+      if (age > (uint32_t)DF_MAXDIST && age < 65536u - 1024u) r = (r & ~(0xFFFFu << (16 * k))) | (stale << (16 * k));
+    }
+    if (r != w) s->head[i] = r;
+  }
+}
+#endif
 
 // 4 bytes at byte x of a register window (x a compile-time constant after unrolling)
 template <int X>
@@ -641,8 +741,7 @@ template <int N>
 __device__ __forceinline__ void ld_run(const MatchShared *s, uint32_t rel, uint32_t (&o)[N]) {
   const uint32_t i = ridx(rel), w = i >> 2, sh = i & 3;
   uint32_t d[N + 1];
-#pragma unroll
-  for (int k = 0; k <= N; ++k) d[k] = s->ring[w + k];
+  ring_dwords<N>(s, w, d);
 #pragma unroll
   for (int k = 0; k < N; ++k) o[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
 }
@@ -706,6 +805,13 @@ __device__ __forceinline__ void walk_extend(Walk &w, const MatchShared *s, const
   // lengths branch-free, so that every load of the run is in flight at once
   uint32_t qw[4];
   ld_run<4>(s, q, qw);
+#ifdef ZT_DF_X_EXT
+  {
+    uint32_t qz[4];
+    ld_run<4>(s, q + 20, qz);
+    qw[0] |= (qz[0] | qz[1] | qz[2] | qz[3]) & ((uint32_t)P.too_far >> 31);
+  }
+#endif
   uint32_t len = eq_len16(qw[0] ^ w.cur, qw[1] ^ w.cur2, qw[2] ^ w.cur3, qw[3] ^ w.cur4);
   // all 16 matched: 16 more bytes per round until a mismatch (or max_len)
   bool more = len == 16;
@@ -746,8 +852,23 @@ __device__ __forceinline__ void walk_pair_step(Walk &a, Walk &b, const MatchShar
   const uint32_t qb = b.q - b.link;
   const bool ha = a.active && a.p - qa <= (uint32_t)DF_MAXDIST;
   const bool hb = b.active && b.p - qb <= (uint32_t)DF_MAXDIST;
-  const uint32_t la = s->prev[ridx(qa)], lb = s->prev[ridx(qb)];
-  const uint32_t oa = ld32(s, qa + a.o), ob = ld32(s, qb + b.o);
+  uint32_t la = s->prev[ridx(qa)], lb = s->prev[ridx(qb)];
+  uint32_t oa = ld32(s, qa + a.o), ob = ld32(s, qb + b.o);
+#if defined(ZT_DF_X_LINK) || defined(ZT_DF_X_FILT)
+  {
+    // (measurement builds: one more read of the kind per hop, its value
+    // masked by a runtime zero -- identical streams, the read's marginal cost)
+    const uint32_t z = (uint32_t)P.too_far >> 31;
+#ifdef ZT_DF_X_LINK
+    la |= (uint32_t)s->prev[ridx(qa + 7)] & z;
+    lb |= (uint32_t)s->prev[ridx(qb + 7)] & z;
+#endif
+#ifdef ZT_DF_X_FILT
+    oa |= ld32(s, qa + a.o + 5) & z;
+    ob |= ld32(s, qb + b.o + 5) & z;
+#endif
+  }
+#endif
   a.q = qa;
   b.q = qb;
 #ifdef ZT_DF_COUNT
@@ -814,8 +935,7 @@ __device__ void search_quad(const MatchShared *s, const DeflateParams &P, uint32
   // bytes [pb - 16, pb + 20) (pb is a multiple of 4; before rel 0 the words
   // are never used: near distances stay <= p)
   uint32_t w[9];
-#pragma unroll
-  for (int i = 0; i < 9; ++i) w[i] = s->ring[ridx(pb - 16 + 4 * i) >> 2];
+  ring_dwords<8>(s, ridx(pb - 16) >> 2, w);
   // positions 0 and 2 walk together, then 1 and 3 with the carry of 0 and 2
   uint32_t out[4];
   uint32_t c0l, c0d, c2l, c2d, cl, cd;
@@ -893,7 +1013,11 @@ __global__ __launch_bounds__(DF_THREADS) void match_kernel(DeflateParams P) {
   key.kmask2 = P.klen >= 8 ? 0xFFFFFFFFu : P.klen == 6 ? 0xFFFFu : P.klen == 5 ? 0xFFu : 0u;
   const uint32_t kext = (uint32_t)P.klen - 1;  // a key at p needs bytes up to p + kext
 
+#ifdef ZT_DF_HEAD16
+  for (uint32_t i = t; i < DF_HSIZE / 2; i += DF_THREADS) s.head[i] = 0x80008000u;  // (rel 0 - 32768: out of reach)
+#else
   for (uint32_t i = t; i < DF_HSIZE; i += DF_THREADS) s.head[i] = kNoHead;
+#endif
   for (uint32_t i = t; i < DF_H4SIZE; i += DF_THREADS) s.head4[i] = kNoHead;
   // the last kext positions of the first sub-chunk read link4 before any
   // link reached their slots: no candidate (not the LDS left by an earlier
@@ -906,10 +1030,7 @@ __global__ __launch_bounds__(DF_THREADS) void match_kernel(DeflateParams P) {
   // run on past the super-chunk into the stream, so that a position at a
   // block end is linked and searched alike whatever the super-chunk size)
   if (DF_HEAD && t < (uint32_t)DF_HEAD && DF_SUB + t < rend) {
-    uint8_t *rb = reinterpret_cast<uint8_t *>(s.ring);
-    const uint8_t b = g[DF_SUB + t];
-    rb[ridx(DF_SUB + t)] = b;
-    if (ridx(DF_SUB + t) < 64) rb[DF_RING + ridx(DF_SUB + t)] = b;
+    ring_put8(&s, ridx(DF_SUB + t), g[DF_SUB + t]);
   }
   const bool g_aligned = (reinterpret_cast<uintptr_t>(g) & 3) == 0;
   for (uint32_t p0 = 0; p0 < re; p0 += DF_SUB) {
@@ -945,6 +1066,9 @@ __global__ __launch_bounds__(DF_THREADS) void match_kernel(DeflateParams P) {
       pml = bend < dend ? bend : dend;
     }
     if (link) hash_keys(&s, inserted, ih, key);
+#ifdef ZT_DF_HEAD16
+    if ((p0 / DF_SUB) % HEAD_SWEEP == 0 && link) head_sweep(&s, p0);
+#endif
     lds_barrier();
     DF_T(t1);
     // wave 0 links the 8-byte-key chains and wave 1 the 4-byte-key table,
@@ -1012,16 +1136,12 @@ __global__ __launch_bounds__(DF_THREADS) void match_kernel(DeflateParams P) {
     }
 #endif
     if (fast) {
-      const uint32_t k0 = ridx(n0);
-      s.ring[(k0 >> 2) + t] = nv;
-      if (k0 == 0 && t < 16) s.ring[DF_RING / 4 + t] = nv;
+      ring_put32(&s, (ridx(n0) >> 2) + t, nv);
     } else if (n0 < re) {
       load_sub(&s, g + n0, n0, (re - n0) < DF_SUB ? (re - n0) : DF_SUB);
     }
     if (hload) {
-      uint8_t *rb = reinterpret_cast<uint8_t *>(s.ring);
-      rb[ridx(hd0 + t)] = hb;
-      if (ridx(hd0 + t) < 64) rb[DF_RING + ridx(hd0 + t)] = hb;
+      ring_put8(&s, ridx(hd0 + t), hb);
     }
   }
 }

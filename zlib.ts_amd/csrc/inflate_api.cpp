@@ -81,7 +81,8 @@ static int batch_two_phase(DeviceCtx *c, const uint8_t *d_in, const std::vector<
     // tokens <= output bytes; every token takes >= 1 input bit
     uint64_t cap = std::max<uint64_t>(65536, 4 * (uint64_t)(n[i] - (index ? index[i] : 0)));
     cap = std::min<uint64_t>(cap, (j.end - j.start) * 8) + 64;
-    cap = std::min<uint64_t>(cap, 1u << 30);
+    // (TokResult::ntok carries flags in bits 30-31: a full slot must not reach them)
+    cap = std::min<uint64_t>(cap, (1u << 30) - 64);
     j.tok_off = tok_total;
     j.tok_cap = (uint32_t)cap;
     j.stop_first = 0;
@@ -384,6 +385,88 @@ int inflate_dev_member(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t index
   return inflate_dev_batch(c, d_in, in_off, &n, &index, 1, 0, out, out_len, end_ip, &st);
 }
 
+// Large host streams with restart points (this engine's deflate output, SURVEY
+// 8(f)): PCIe overlapped with the decode, as deflate_raw_pipelined does for
+// deflate.  The input is cut after restart markers (00 00 00 FF FF 00 00 00
+// FF FF: empty stored blocks, no match reaches behind them) found by the host
+// near every kInfPiece-th byte; piece i + 1 is uploaded while piece i is
+// decoded and piece i - 1's bytes come back (pipeline_h2d_d2h).  A non-final
+// piece gets an empty final stored block (01 00 00 FF FF) after it on the
+// device and is decoded as a stream of its own: it must end exactly there,
+// which certifies that the cut is a real block boundary (a decode from a true
+// block start is deterministic -- reaching the appended block's end any
+// other way is impossible without consuming real block ends); a piece whose
+// matches reach behind its start fails in the segment decoder.  Any failure
+// -- no marker, a piece the segment path cannot decode, an output past the
+// host bound -- returns 1 and the caller decodes the whole stream in one call
+// (tests/test_gpu_api_pipeline.py: identical output and end position).
+static constexpr size_t kInfPipeMin = 32u << 20;
+static constexpr size_t kInfPiece = 32u << 20;
+
+static int inflate_raw_pipelined(DeviceCtx *c, const uint8_t *in, size_t n, size_t index, uint8_t **out,
+                                 size_t *out_len, size_t *end_ip) {
+  static const uint8_t kMarker[10] = {0, 0, 0, 0xFF, 0xFF, 0, 0, 0, 0xFF, 0xFF};
+  static const uint8_t kFinal[5] = {1, 0, 0, 0xFF, 0xFF};
+  const size_t m = n - index;
+  const size_t piece = std::min(std::max(m / 16, (size_t)8 << 20), kInfPiece);
+  std::vector<size_t> cut{index};
+  for (size_t t = index + piece; t + piece / 2 < n; t = cut.back() + piece) {
+    const size_t lo = std::max(t, cut.back()) - 10, hi = std::min(n, t + (8u << 20));
+    const void *q = memmem(in + lo, hi - lo, kMarker, sizeof kMarker);
+    if (!q) break;
+    const size_t p = (size_t)((const uint8_t *)q - in) + sizeof kMarker;
+    if (p + piece / 2 >= n) break;  // (the last piece keeps at least half a piece)
+    cut.push_back(p);
+  }
+  cut.push_back(n);
+  const size_t np = cut.size() - 1;
+  if (np < 2) return 1;
+  void *d_in, *d_out;
+  ZT_TRY(scratch(c, 0, m + 64 * np + 256, &d_in));
+  // outputs of up to 4x the input (the host bound below); past it: one call
+  const size_t cap = std::max<size_t>(4 * m, 64u << 20);
+  ZT_TRY(scratch(c, 22, cap, &d_out));
+  uint8_t *h = host_out(cap);  // (pages past the output are never touched)
+  if (!h) return set_error(ZT_E_NOMEM, "host allocation failed");
+  auto d_piece = [&](size_t i) { return (uint8_t *)d_in + (cut[i] - index) + 64 * i; };
+  size_t off = 0, eip_last = 0;
+  size_t total = 0;
+  const int rc = pipeline_h2d_d2h(
+      c, np, [&](size_t i) { return PipePiece{in + cut[i], d_piece(i), cut[i + 1] - cut[i]}; },
+      [&](size_t i, const void **d_res, size_t *n_res) -> int {
+        const size_t len = cut[i + 1] - cut[i];
+        const bool last = i + 1 == np;
+        if (!last) ZT_HIP(hipMemcpyAsync(d_piece(i) + len, kFinal, sizeof kFinal, hipMemcpyHostToDevice, c->stream));
+        const size_t pn = last ? len : len + sizeof kFinal;
+        uint8_t *d_o = (uint8_t *)d_out + off;
+        size_t ol = 0, eip = 0;
+        // the piece's output capacity: 4x its input first (the device chain's
+        // descriptors are sized from it), everything left if that is short
+        int seg = inflate_segments_dev(c, d_piece(i), pn, 0, &d_o, std::min(cap - off, 4 * pn + (1u << 20)), &ol,
+                                       &eip, c->stream);
+        if (seg < 0 && 4 * pn + (1u << 20) < cap - off)
+          seg = inflate_segments_dev(c, d_piece(i), pn, 0, &d_o, cap - off, &ol, &eip, c->stream);
+        // (no sync points in the piece: the speculative general decoder)
+        if (seg >= 1) seg = inflate_general_dev(c, d_piece(i), pn, 0, &d_o, cap - off, &ol, &eip, c->stream);
+        if (seg != 0) return seg < 0 ? seg : set_error(ZT_E_INTERNAL, "pipelined inflate: piece not decoded");
+        if (!last && eip != pn) return set_error(ZT_E_INTERNAL, "pipelined inflate: a cut is not a block boundary");
+        eip_last = eip;
+        *d_res = d_o;
+        *n_res = ol;
+        off += ol;
+        return ZT_OK;
+      },
+      h, cap, &total);
+  if (rc) {
+    zt_free(h);
+    return 1;
+  }
+  *out = h;
+  *out_len = total;
+  if (end_ip) *end_ip = cut[np - 1] + eip_last;
+  return ZT_OK;
+}
+
 }  // namespace zt
 
 using namespace zt;
@@ -398,6 +481,9 @@ int zt_inflate_raw(const uint8_t *in, size_t n, size_t index, const zt_inflate_o
     DeviceCtx *c;
     ZT_TRY(get_ctx(&c));
     std::lock_guard<std::recursive_mutex> ctx_lock(c->mu);
+    static const bool no_pipe = getenv("ZT_INF_NOPIPE") != nullptr;  // (A/B measurement and the identity test)
+    if (!no_pipe && n - index >= kInfPipeMin && inflate_raw_pipelined(c, in, n, index, out, out_len, end_ip) == ZT_OK)
+      return ZT_OK;
     void *d_in;
     ZT_TRY(scratch(c, 0, n, &d_in));
     ZT_TRY(upload(c, d_in, in, n, c->stream));

@@ -63,6 +63,7 @@ bool inf_debug() {
 // this engine's units are one DEFLATE block of ZT_DF_GROUP parse blocks
 // (deflate.hip): <= 1 token per byte
 constexpr uint32_t kUnitTokCap = ZT_DF_BLOCK * ZT_DF_GROUP + 64;
+static_assert(kUnitTokCap < (1u << 30), "token counts stay below TokResult::ntok's flag bits");
 
 // sync point = byte after an aligned 00 00 FF FF; list entry = pos << 1 | restart
 // One 16-byte aligned chunk per lane, loaded as one 16-byte word; the 8 bytes
@@ -628,13 +629,23 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   static const bool host_chain = getenv("ZT_INF_HOST_CHAIN") != nullptr;
   const uint32_t max_seg = (uint32_t)std::min<uint64_t>(tot_h[2] + 1, units);
   const uint64_t desc_cap = (uint64_t)out_cap + 512ull * max_seg + 2048;
+  // The descriptors are sized from the caller's capacity here (the decoded
+  // size is known only after the chain), and the scratch cache only grows: a
+  // generous capacity takes the device chain only when its descriptors fit
+  // what slot 3 already holds or 8 bytes per input byte (output up to 4x the
+  // input); otherwise, and when the slot cannot grow, the host walks the chain
+  // and sizes them from the real total.
+  const bool desc_fits = desc_cap * 2 <= c->buf_size[3] || desc_cap * 2 <= 8ull * n + 4ull * (512ull * max_seg + 2048);
   if (*d_out_io && !check && !inf_debug() && !host_chain && max_seg <= CH_MAXS && units <= CH_MAXU &&
-      out_cap <= (64ull << 30)) {
+      out_cap <= (64ull << 30) && desc_fits) {
     void *d_chain, *d_desc;
     const size_t chain_bytes = align256(units * sizeof(ChainUnit)), seg_bytes = align256(max_seg * sizeof(SegJob));
     const size_t ust_bytes = align256(units * 4), st_bytes = align256(max_seg * 4);
     ZT_TRY(scratch(c, 7, chain_bytes + seg_bytes + ust_bytes + st_bytes + 256, &d_chain));
-    ZT_TRY(scratch(c, 3, desc_cap * 2, &d_desc));
+    if (scratch(c, 3, desc_cap * 2, &d_desc) != ZT_OK) {
+      (void)hipGetLastError();  // (the failed allocation's sticky error)
+      goto host_walk;
+    }
     uint8_t *cb = static_cast<uint8_t *>(d_chain);
     ChainUnit *d_cu = reinterpret_cast<ChainUnit *>(cb);
     SegJob *d_sj = reinterpret_cast<SegJob *>(cb + chain_bytes);
@@ -683,6 +694,7 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
     // not the common case: the host walks the chain (the kernels above did nothing)
     ZT_TRY(timing_begin(c, s, 2));
   }
+host_walk:
   TokResult *res = reinterpret_cast<TokResult *>(pin + restart_bytes);
   ZT_HIP(hipMemcpyAsync(pin, d_restart, nsync, hipMemcpyDeviceToHost, s));
   ZT_HIP(hipMemcpyAsync(res, d_res, units * sizeof(TokResult), hipMemcpyDeviceToHost, s));

@@ -303,6 +303,7 @@ int zt_unzip(const uint8_t *in, size_t n, int verify, uint8_t **out, size_t *out
     std::sort(starts.begin(), starts.end());
     std::vector<size_t> in_off(m, 0), nn(m, n), idx(m), bl(m), eip(m);
     std::vector<uint8_t *> bp(m, nullptr);
+    Freer bp_freer{bp};  // (every early return frees what the batch allocated; handed-on pointers are nulled)
     // (a batch that fails as a whole -- device memory, HIP -- leaves kNotRun)
     constexpr int kNotRun = -0x7FFF;
     std::vector<int> st(m, kNotRun);
@@ -356,9 +357,11 @@ int zt_unzip(const uint8_t *in, size_t n, int verify, uint8_t **out, size_t *out
         inflate_error(st[k], 0);
         snprintf(ent[i].message, sizeof ent[i].message, "%s", zt_last_error_message());
         zt_free(bp[k]);
+        bp[k] = nullptr;
         continue;
       }
       o[i] = bp[k];
+      bp[k] = nullptr;
       ol[i] = bl[k];
     }
   }

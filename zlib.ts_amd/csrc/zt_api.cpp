@@ -559,7 +559,7 @@ int zt_release_scratch(void) {
   ZT_TRY(get_ctx(&c));
   std::lock_guard<std::recursive_mutex> ctx_lock(c->mu);
   ZT_HIP(hipDeviceSynchronize());
-  for (int k = 0; k < 22; ++k) {
+  for (int k = 0; k < DeviceCtx::kSlots; ++k) {
     if (c->d_buf[k]) ZT_HIP(hipFree(c->d_buf[k]));
     c->d_buf[k] = nullptr;
     c->buf_size[k] = 0;

@@ -52,9 +52,11 @@ struct DeviceCtx {
   uint32_t *d_crc_shift = nullptr;  // checksum.hip merge constants (crc_shift_tables)
   CkAcc *d_ck_acc = nullptr;        // checksum merge accumulators (zeroed once, left zeroed by every call)
   // scratch
-  void *d_buf[22] = {};  // slot 8: checksum segment partials; 10-17: general inflate (inflate_gen.hip);
-                         // 20: segment inflate's sync-point sort (inflate_seg.hip); 21: stored runs
-  size_t buf_size[22] = {};
+  static constexpr int kSlots = 23;
+  void *d_buf[kSlots] = {};  // slot 8: checksum segment partials; 10-17: general inflate (inflate_gen.hip);
+                             // 20: segment inflate's sync-point sort (inflate_seg.hip); 21: stored runs;
+                             // 22: pipelined host inflate's output (inflate_api.cpp)
+  size_t buf_size[kSlots] = {};
   // second stream: checksums run beside the deflate pipeline in the containers
   hipStream_t aux = nullptr;
   hipEvent_t aux_ev = nullptr;
