@@ -135,6 +135,24 @@ def pmc_traffic(kernel, n):
     return int(k["traffic_bytes"])
 
 
+def pmc_lds(kernel, n):
+    """The kernel's binding resource (SURVEY 8(d) honesty note: LZ77 match
+    finding is LDS-bound, not HBM-bound): the LDS array's busy fraction of
+    the kernel's CU-cycles and the bank-conflict share of those cycles, from
+    profiles/pmc_lds.json (tools/pmc_lds.py over a rocprofv3 SQ pass of this
+    workload) -- or None when it was measured on other kernel sources."""
+    path = os.path.join(HERE, "profiles", "pmc_lds.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if d.get("kernel") != kernel or n != 1 << 30 or d.get("source_sha256") != source_digest():
+        return None
+    return {"bound": "lds", "busy_frac": d["busy_frac"], "bank_conflict_frac": d["bank_conflict_frac"],
+            "source": "profiles/pmc_lds.json"}
+
+
 def host_info():
     model = None
     try:
@@ -345,7 +363,8 @@ def run_rank(args):
         "deflate_GiBps": round(n / (pipe_ms * 1e-3) / 2**30, 3) if pipe_ms else None,
         "roofline": {"bound": "hbm", "kernel": "match_kernel", "achieved": round(achieved, 3),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
-                     "traffic": pmc_traffic("match_kernel", n)},
+                     "traffic": pmc_traffic("match_kernel", n),
+                     "lds": pmc_lds("match_kernel", n)},
         "devices_visible": ndev,
     }
     if args.mode != "c3":

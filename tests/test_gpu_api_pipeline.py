@@ -79,8 +79,8 @@ def _device_inflate(zt, torch, s, n_out):
 
 @pytest.mark.parametrize("n,kind,tail", [
     ((96 << 20) + 5, "mixed", b""),                 # ~6 pieces of 8 MiB of stream
-    ((200 << 20) + 4099, "wordsalad", b""),         # pieces of 8-32 MiB, ragged last
-    ((224 << 20) + 17, "structured", b"\x07" * 33),  # trailing bytes after the stream
+    ((224 << 20) + 4099, "wordsalad", b""),         # pieces of 8-32 MiB, ragged last
+    ((160 << 20) + 17, "structured", b"\x07" * 33),  # trailing bytes after the stream
 ])
 def test_pipelined_inflate_equals_single_call(zt, n, kind, tail):
     import numpy as np
@@ -90,7 +90,7 @@ def test_pipelined_inflate_equals_single_call(zt, n, kind, tail):
     zt.synth_dev(kind, 9, d_in.data_ptr(), n)
     host = d_in.cpu().numpy()
     s = _device_stream(zt, torch, d_in, n, 6)
-    assert len(s) >= 32 << 20 or kind == "structured"
+    assert len(s) >= 32 << 20  # (the pipelined path's threshold)
     back, ip = zt.inflate_raw(s + tail)
     assert ip == len(s) and len(back) == n
     assert np.array_equal(np.frombuffer(back, dtype=np.uint8), host)

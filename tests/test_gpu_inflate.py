@@ -289,3 +289,34 @@ def test_two_phase_block_shapes(zt, oracle):
         s = b"".join(parts)
         out, ip = zt.inflate_raw(s)
         assert out == d and ip == len(s), (level, strategy)
+
+
+def test_generous_capacity_bounds_descriptor_scratch(zt):
+    """zt_inflate_dev with an output capacity far above the decoded size
+    (inflate_seg.hip): the device chain sizes its descriptors from the
+    capacity, so it is taken only when they fit 8 bytes per input byte (or
+    what the scratch already holds); otherwise the host walks the chain and
+    sizes them from the real total.  The output is the same either way and
+    the cached device scratch stays proportional to the stream, not to the
+    capacity."""
+    import torch
+
+    n = 24 << 20
+    d_in = torch.empty(n, dtype=torch.uint8, device="cuda")
+    zt.synth_dev("mixed", 13, d_in.data_ptr(), n)
+    dp = zt.DeflatePlan(n, level=6)
+    d_c = torch.empty(zt.deflate_bound(n), dtype=torch.uint8, device="cuda")
+    clen = dp.run(d_in.data_ptr(), n, d_c.data_ptr())
+    dp.close()
+    zt.release_scratch()
+    cap = 8 << 30  # 8 GiB of (virtual) capacity for a 24 MiB output
+    d_out = torch.empty(n + (1 << 20), dtype=torch.uint8, device="cuda")
+    ip_ = zt.InflatePlan(clen, cap)
+    # the output buffer holds n bytes + 1 MiB: the decode writes n bytes, the
+    # capacity passed only sizes the descriptor scratch
+    ol, ip = ip_.run(d_c.data_ptr(), clen, d_out.data_ptr(), cap)
+    ip_.close()
+    assert ol == n and ip == clen
+    assert torch.equal(d_out[:n], d_in)
+    dev_bytes, _ = zt.scratch_bytes()
+    assert dev_bytes < 40 * n, dev_bytes  # not 2 x 8 GiB of descriptors

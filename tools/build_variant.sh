@@ -6,9 +6,11 @@ set -e
 NAME=$1; shift
 cd "$(dirname "$0")/../zlib.ts_amd"
 OUT=build/${VAR_PREFIX:-var_}$NAME; mkdir -p $OUT
+pids=()
 for f in csrc/*.hip csrc/*.cpp; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-function "$@" -c -o $OUT/$(basename $f).o $f &
+  pids+=($!)
 done
-wait
+for p in "${pids[@]}"; do wait $p || { echo "build_variant: a compile failed" >&2; exit 1; }; done
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -shared -o $OUT/libzt.so $OUT/*.o
 echo built $OUT/libzt.so

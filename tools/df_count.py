@@ -14,4 +14,5 @@ for kind in sys.argv[1:]:
     zt.lib.zt_debug_df_count(buf)
     v = list(buf)
     print(kind, 'pair-steps/wave', v[0], 'lane hops', v[1], 'extends', v[2], 'hops/position %.2f' % (v[1] / n),
-          'lane-util %.2f' % (v[1] / max(1, v[0] * 128)), flush=True)
+          'lane-util %.2f' % (v[1] / max(1, v[0] * 128)), 'extend passes/step %.2f' % (v[3] / max(1, v[0])),
+          'lanes/pass %.1f' % (v[2] / max(1, v[3])), flush=True)

@@ -52,7 +52,7 @@ __device__ unsigned long long g_bk_time[8];  // debug: block_kernel phase cycles
 #define DF_T(v) (void)0
 #endif
 #ifdef ZT_DF_COUNT
-__device__ unsigned long long g_df_count[4];  // debug: pair steps (per wave), lane hops, extends
+__device__ unsigned long long g_df_count[4];  // debug: pair steps (per wave), lane hops, extends (lanes), extends (waves)
 #endif
 
 #ifndef ZT_DF_BLOCK
@@ -786,6 +786,33 @@ __device__ __forceinline__ void walk_init(Walk &w, const MatchShared *s, const D
   }
 }
 
+#ifdef ZT_DF_EQ2
+// equal leading bytes (0..16) of four XORed words: the first differing bit
+// of each word (v_ffbl: ~0 for none), offset by the word's place with
+// unsigned saturation (none stays ~0), the least of them -- 11 VALU; inline
+// asm because the compiler rewrites ffs of a possibly-zero word into
+// compares and selects
+__device__ __forceinline__ uint32_t ffbl_raw(uint32_t x) {
+  uint32_t r;
+  asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+template <uint32_t B>
+__device__ __forceinline__ uint32_t add_sat(uint32_t a) {
+  uint32_t r;
+  asm("v_add_u32_e64 %0, %1, %2 clamp" : "=v"(r) : "v"(a), "v"(B));
+  return r;
+}
+__device__ __forceinline__ uint32_t min3_u32(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_min3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ uint32_t eq_len16(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) {
+  const uint32_t m = min3_u32(ffbl_raw(x0), add_sat<32>(ffbl_raw(x1)), add_sat<64>(ffbl_raw(x2)));
+  return min3_u32(m, add_sat<96>(ffbl_raw(x3)), 128u) >> 3;
+}
+#else
 // equal leading bytes (0..16) of four XORed words, without branches
 __device__ __forceinline__ uint32_t eq_len16(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) {
   const uint32_t l0 = min((uint32_t)(__ffs(x0) - 1) >> 3, 4u), l1 = min((uint32_t)(__ffs(x1) - 1) >> 3, 4u);
@@ -794,24 +821,20 @@ __device__ __forceinline__ uint32_t eq_len16(uint32_t x0, uint32_t x1, uint32_t 
   const uint32_t t1 = l1 == 4 ? 4 + t2 : l1;
   return l0 == 4 ? 4 + t1 : l0;
 }
+#endif
 
 // a candidate q that passed the one-word filter: its length from byte 0
 // (the filter checked at most 4 bytes) and keep the longest
 __device__ __forceinline__ void walk_extend(Walk &w, const MatchShared *s, const DeflateParams &P, uint32_t q) {
 #ifdef ZT_DF_COUNT
   atomicAdd(&g_df_count[2], 1ull);
+  // (wave-level executions of the measurement: its first active lane counts)
+  if ((int)(threadIdx.x & 63) == __ffsll((unsigned long long)__ballot(1)) - 1) atomicAdd(&g_df_count[3], 1ull);
 #endif
   // the first 16 bytes: q's words in one run of loads, p's from registers;
   // lengths branch-free, so that every load of the run is in flight at once
   uint32_t qw[4];
   ld_run<4>(s, q, qw);
-#ifdef ZT_DF_X_EXT
-  {
-    uint32_t qz[4];
-    ld_run<4>(s, q + 20, qz);
-    qw[0] |= (qz[0] | qz[1] | qz[2] | qz[3]) & ((uint32_t)P.too_far >> 31);
-  }
-#endif
   uint32_t len = eq_len16(qw[0] ^ w.cur, qw[1] ^ w.cur2, qw[2] ^ w.cur3, qw[3] ^ w.cur4);
   // all 16 matched: 16 more bytes per round until a mismatch (or max_len)
   bool more = len == 16;
@@ -839,6 +862,7 @@ __device__ __forceinline__ void walk_extend(Walk &w, const MatchShared *s, const
   }
 }
 
+
 // one hop of two walks: every LDS load of both hops is issued before any is
 // used (the walks are latency-bound pointer chases), then the checks.  Per
 // hop two loads: the link and the filter word.
@@ -852,23 +876,8 @@ __device__ __forceinline__ void walk_pair_step(Walk &a, Walk &b, const MatchShar
   const uint32_t qb = b.q - b.link;
   const bool ha = a.active && a.p - qa <= (uint32_t)DF_MAXDIST;
   const bool hb = b.active && b.p - qb <= (uint32_t)DF_MAXDIST;
-  uint32_t la = s->prev[ridx(qa)], lb = s->prev[ridx(qb)];
-  uint32_t oa = ld32(s, qa + a.o), ob = ld32(s, qb + b.o);
-#if defined(ZT_DF_X_LINK) || defined(ZT_DF_X_FILT)
-  {
-    // (measurement builds: one more read of the kind per hop, its value
-    // masked by a runtime zero -- identical streams, the read's marginal cost)
-    const uint32_t z = (uint32_t)P.too_far >> 31;
-#ifdef ZT_DF_X_LINK
-    la |= (uint32_t)s->prev[ridx(qa + 7)] & z;
-    lb |= (uint32_t)s->prev[ridx(qb + 7)] & z;
-#endif
-#ifdef ZT_DF_X_FILT
-    oa |= ld32(s, qa + a.o + 5) & z;
-    ob |= ld32(s, qb + b.o + 5) & z;
-#endif
-  }
-#endif
+  const uint32_t la = s->prev[ridx(qa)], lb = s->prev[ridx(qb)];
+  const uint32_t oa = ld32(s, qa + a.o), ob = ld32(s, qb + b.o);
   a.q = qa;
   b.q = qb;
 #ifdef ZT_DF_COUNT
@@ -1794,6 +1803,23 @@ __global__ __launch_bounds__(64, ZT_OP_MINW) void optparse_kernel(DeflateParams 
               // one add3 of pre-shifted terms (exact modulo 2^32: the
               // unshifted value is below 2^23)
               const uint32_t base9 = (uint32_t)(dc + 0x8000 - (int)C1) << 9;
+#ifdef ZT_OP_SPARSE
+              // every cut length up to 10, then the longest of each length
+              // symbol's range (the same length price: 12, 14, 16, 18, 22,
+              // 24), and the full match itself
+              constexpr uint32_t kCuts[14] = {3, 4, 5, 6, 7, 8, 9, 10, 12, 14, 16, 18, 22, 24};
+              static_assert(OP_SHORT == 24, "the sparse cut list ends at 24");
+#pragma unroll
+              for (int j = 0; j < 14; j += 2) {
+                const uint32_t l = kCuts[j], l2 = kCuts[j + 1];
+                const uint32_t ka = base9 + cr9[l] + lk[l], kb = base9 + cr9[l2] + lk[l2];
+                key = op_min3(key, l <= L ? ka : 0xFFFFFFFFu, l2 <= L ? kb : 0xFFFFFFFFu);
+              }
+              {
+                const uint32_t kl = ((uint32_t)(dc + 0x8000 + c_far) << 9) | (Lc & 511);
+                key = (L > 10 && kl < key) ? kl : key;
+              }
+#else
 #pragma unroll
               for (uint32_t l = 3; l < OP_SHORT; l += 2) {
                 const uint32_t ka = base9 + cr9[l] + lk[l], kb = base9 + cr9[l + 1] + lk[l + 1];
@@ -1803,6 +1829,7 @@ __global__ __launch_bounds__(64, ZT_OP_MINW) void optparse_kernel(DeflateParams 
                 const uint32_t kl = ((uint32_t)(dc + 0x8000 + c_far) << 9) | (Lc & 511);
                 key = (L > OP_SHORT && kl < key) ? kl : key;
               }
+#endif
               const uint32_t choice = key & 511;
               const int best = (int)(key >> 9) - 0x8000;
               C1 += (uint32_t)best;
