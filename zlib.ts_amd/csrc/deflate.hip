@@ -247,7 +247,7 @@ __device__ __forceinline__ uint32_t res_byte(uint32_t r) { return r >> 24; }
 //     from registers (each thread 128 consecutive positions); a repeat of L
 //     bytes gives ~L / 16 hits (the pair's other position, before or after,
 //     within a match distance).  CL_HITS hits or more -> search.
-//  C. the whole block's byte histogram (counted from the registers stage B
+//  C. the block's byte histogram (every 3rd byte, from the registers stage B
 //     loaded): a block whose order-0 entropy would let an ideal literal coder
 //     save more than CL_SAVE over the stored form is searched (a skewed
 //     block -- 7.85..7.98 bits -- or compressible bytes outside the sample).
@@ -257,6 +257,7 @@ __device__ __forceinline__ uint32_t res_byte(uint32_t r) { return r >> 24; }
 constexpr float CL_ENTROPY = 7.85f;  // uniform bytes: ~7.955 from a 4096-byte sample
 constexpr uint32_t CL_HITS = 8;
 constexpr float CL_SAVE = 0.002f;  // C: largest saving an ideal literal coder may forgo
+constexpr int CL_STRIDE = 3;       // C: every 3rd byte counted
 constexpr uint32_t CL_TABLE = 8192;
 constexpr uint32_t CL_EMPTY = 0xFFFFFFFFu;
 struct ClassifyShared {
@@ -264,6 +265,7 @@ struct ClassifyShared {
   uint32_t hist[256];
   float part[4];
   uint32_t hits[4];
+  float cnt[4][2];  // stage C: bytes counted, bins used (per wave)
 };
 
 // 4 stream bytes at g + off (off >= 0 relative to a possibly unaligned g);
@@ -397,9 +399,11 @@ __global__ __launch_bounds__(256) void classify_kernel(DeflateParams P) {
 #pragma unroll
       for (int j = 0; j < 34; ++j) w[j] = cl_gword(g, (int64_t)(lo + k0 + 4 * j), n);
     }
-    // the whole block's byte histogram (stage A saw a 4 KiB sample only)
+    // the block's byte histogram over every 3rd byte (stage A saw a 4 KiB
+    // sample only; a stride prime to 2 sees every byte lane of 2-, 4- and
+    // 8-byte records; all 32 KiB took 0.23 ms per GiB of LDS atomics)
 #pragma unroll
-    for (int k = 0; k < 128; ++k)
+    for (int k = 0; k < 128; k += CL_STRIDE)
       if (k0 + (uint32_t)k < blen) atomicAdd(&s->hist[(w[k >> 2] >> (8 * (k & 3))) & 0xFF], 1u);
 #pragma unroll
     for (int k = 0; k < 128; ++k) {
@@ -417,18 +421,30 @@ __global__ __launch_bounds__(256) void classify_kernel(DeflateParams P) {
   for (int off = 32; off; off >>= 1) hits += __shfl_xor(hits, off, 64);
   if ((t & 63) == 0) s->hits[t >> 6] = hits;
   __syncthreads();
-  // C. the whole block's order-0 entropy: an ideal literal coder (which no
-  // Huffman code beats) + a 32-byte header must not save more than
-  // CL_SAVE of the block over the stored form, or the block is searched
-  // (uniform bytes: ~7.994 bits per byte over 32 KiB, the cut ~7.98)
+  // C. the block's order-0 entropy (Miller-Madow: the sample's plug-in
+  // estimate + (bins used - 1) / (2 N ln 2), its bias): an ideal literal
+  // coder (which no Huffman code beats) + a 32-byte header must not save more
+  // than CL_SAVE of the block over the stored form, or the block is searched
+  // (uniform bytes: ~8.00 bits per byte, the cut ~7.98)
   const float cb = (float)s->hist[t];
-  float eb = cb > 0.f ? cb * __log2f(cb) : 0.f;
-  for (int off = 32; off; off >>= 1) eb += __shfl_xor(eb, off, 64);
+  float eb = cb > 0.f ? cb * __log2f(cb) : 0.f, nb = cb, kb = cb > 0.f ? 1.f : 0.f;
+  for (int off = 32; off; off >>= 1) {
+    eb += __shfl_xor(eb, off, 64);
+    nb += __shfl_xor(nb, off, 64);
+    kb += __shfl_xor(kb, off, 64);
+  }
   __syncthreads();  // (every hist read done before part[] is rewritten below)
-  if ((t & 63) == 0) s->part[t >> 6] = eb;
+  if ((t & 63) == 0) {
+    s->part[t >> 6] = eb;
+    s->cnt[t >> 6][0] = nb;
+    s->cnt[t >> 6][1] = kb;
+  }
   __syncthreads();
   if (t == 0) {
-    const float hb = __log2f((float)blen) - (s->part[0] + s->part[1] + s->part[2] + s->part[3]) / (float)blen;
+    const float n = s->cnt[0][0] + s->cnt[1][0] + s->cnt[2][0] + s->cnt[3][0];
+    const float k = s->cnt[0][1] + s->cnt[1][1] + s->cnt[2][1] + s->cnt[3][1];
+    const float hb = __log2f(n) - (s->part[0] + s->part[1] + s->part[2] + s->part[3]) / n +
+                     (k - 1.f) / (2.f * n * 0.69314718f);
     const bool flat = hb * (float)blen * 0.125f + 32.f >= (1.0f - CL_SAVE) * (float)blen;
     const bool st = flat && (s->hits[0] + s->hits[1] + s->hits[2] + s->hits[3]) < CL_HITS;
     P.store[blk] = st ? 1 : 0;
@@ -449,6 +465,10 @@ struct MatchShared {
   uint32_t head4[DF_H4SIZE];        // newest position (rel) per 4-byte-key bucket
   uint16_t link4[DF_SUB];           // position p of the sub-chunk: distance to the newest earlier
                                     // position of its 4-byte-key bucket (0 = none), at p % DF_SUB
+#ifdef ZT_DF_MQ
+  uint32_t mq[DF_THREADS / 64][256];  // per wave: candidates to measure (q | walk slot << 18), a ring
+  uint32_t mr[DF_THREADS / 64][128];  // per wave and walk slot: best (length << 15 | 0x7FFF - distance)
+#endif
   uint32_t dummy[4];                // exchange / link targets of lanes past the end (branch-free chain_link)
   uint32_t linked;                  // positions below are linked (chain_link -> searching waves)
   uint32_t linked4;                 // positions below have their 4-byte links
@@ -493,7 +513,7 @@ __device__ __forceinline__ uint32_t ld8(const MatchShared *s, uint32_t rel) {
 __device__ __forceinline__ uint32_t ld32(const MatchShared *s, uint32_t rel) {
   const uint32_t i = ridx(rel);
   const uint2 v = ring_pair(s, i >> 2);
-  return __builtin_amdgcn_alignbyte(v.y, v.x, i & 3);
+  return __builtin_amdgcn_alignbyte(v.y, v.x, i);  // (v_alignbyte_b32 reads the shift's low 2 bits only)
 }
 // chain key at p: the first klen bytes (kmask: bytes 0-3, kmask2: bytes 4-7)
 struct Key {
@@ -739,7 +759,7 @@ struct Walk {
 // ring's end keeps up to 15 words contiguous): n + 1 dword loads, no wrap math
 template <int N>
 __device__ __forceinline__ void ld_run(const MatchShared *s, uint32_t rel, uint32_t (&o)[N]) {
-  const uint32_t i = ridx(rel), w = i >> 2, sh = i & 3;
+  const uint32_t i = ridx(rel), w = i >> 2, sh = i;  // (v_alignbyte_b32 reads the shift's low 2 bits only)
   uint32_t d[N + 1];
   ring_dwords<N>(s, w, d);
 #pragma unroll
@@ -786,12 +806,13 @@ __device__ __forceinline__ void walk_init(Walk &w, const MatchShared *s, const D
   }
 }
 
-#ifdef ZT_DF_EQ2
 // equal leading bytes (0..16) of four XORed words: the first differing bit
 // of each word (v_ffbl: ~0 for none), offset by the word's place with
-// unsigned saturation (none stays ~0), the least of them -- 11 VALU; inline
-// asm because the compiler rewrites ffs of a possibly-zero word into
-// compares and selects
+// unsigned saturation (none stays ~0; the last word's by a min with 32, so
+// that no constant needs a register), the least of them -- 11 VALU (round
+// 4's per-word selects: 17, and the measurement is the walk's VALU-heaviest
+// part: match 22.4 -> 20.4 ms per GiB, streams identical); inline asm because
+// the compiler rewrites ffs of a possibly-zero word into compares and selects
 __device__ __forceinline__ uint32_t ffbl_raw(uint32_t x) {
   uint32_t r;
   asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
@@ -800,7 +821,8 @@ __device__ __forceinline__ uint32_t ffbl_raw(uint32_t x) {
 template <uint32_t B>
 __device__ __forceinline__ uint32_t add_sat(uint32_t a) {
   uint32_t r;
-  asm("v_add_u32_e64 %0, %1, %2 clamp" : "=v"(r) : "v"(a), "v"(B));
+  static_assert(B <= 64, "an inline constant (VOP3 takes no literal here)");
+  asm("v_add_u32_e64 %0, %1, %2 clamp" : "=v"(r) : "v"(a), "i"(B));
   return r;
 }
 __device__ __forceinline__ uint32_t min3_u32(uint32_t a, uint32_t b, uint32_t c) {
@@ -810,18 +832,9 @@ __device__ __forceinline__ uint32_t min3_u32(uint32_t a, uint32_t b, uint32_t c)
 }
 __device__ __forceinline__ uint32_t eq_len16(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) {
   const uint32_t m = min3_u32(ffbl_raw(x0), add_sat<32>(ffbl_raw(x1)), add_sat<64>(ffbl_raw(x2)));
-  return min3_u32(m, add_sat<96>(ffbl_raw(x3)), 128u) >> 3;
+  const uint32_t l3 = min(ffbl_raw(x3), 32u) + 96u;  // (<= 128: all 16 bytes equal)
+  return min(m, l3) >> 3;
 }
-#else
-// equal leading bytes (0..16) of four XORed words, without branches
-__device__ __forceinline__ uint32_t eq_len16(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) {
-  const uint32_t l0 = min((uint32_t)(__ffs(x0) - 1) >> 3, 4u), l1 = min((uint32_t)(__ffs(x1) - 1) >> 3, 4u);
-  const uint32_t l2 = min((uint32_t)(__ffs(x2) - 1) >> 3, 4u), l3 = min((uint32_t)(__ffs(x3) - 1) >> 3, 4u);
-  const uint32_t t2 = l2 == 4 ? 4 + l3 : l2;
-  const uint32_t t1 = l1 == 4 ? 4 + t2 : l1;
-  return l0 == 4 ? 4 + t1 : l0;
-}
-#endif
 
 // a candidate q that passed the one-word filter: its length from byte 0
 // (the filter checked at most 4 bytes) and keep the longest
@@ -847,21 +860,53 @@ __device__ __forceinline__ void walk_extend(Walk &w, const MatchShared *s, const
     more = l == 16;
   }
   if (len > w.max_len) len = w.max_len;
-  if (len >= 3 && len > w.best_len) {
-    w.best_len = len;
-    w.best_dist = w.p - q;
-    if ((int)len >= P.nice_len || len >= w.max_len) {
-      w.active = false;
-      return;
-    }
-    if (len >= 4) {
-      w.o = len - 3;
-      w.omask = 0xFFFFFFFFu;
-      w.pw = ld32(s, w.p + w.o);
-    }
-  }
+  // branch-free update (selects instead of nested exec-mask branches: the
+  // pass runs with a few lanes of the wave, and every branch of the nest is
+  // taken by one of them: match 21.0 -> 20.3 ms per GiB, streams identical)
+  const bool upd = len >= 3 && len > w.best_len;
+  const bool stop = upd && ((int)len >= P.nice_len || len >= w.max_len);
+  const bool newo = upd && !stop && len >= 4;
+  w.best_len = upd ? len : w.best_len;
+  w.best_dist = upd ? w.p - q : w.best_dist;
+  w.active = w.active && !stop;
+  w.o = newo ? len - 3 : w.o;
+  w.omask = newo ? 0xFFFFFFFFu : w.omask;
+  const uint32_t npw = ld32(s, w.p + w.o);
+  w.pw = newo ? npw : w.pw;
 }
 
+
+#ifdef ZT_DF_MQ
+// Candidate measurement through a per-wave queue.  A hop's candidate (it
+// passed the filter) is appended to the wave's queue instead of being
+// measured at once -- at once, the wave ran the measurement whenever any of
+// its 128 walks had one: 1.5 passes per pair step with 4.7 lanes each on
+// text, about three times the VALU of the hops themselves.  Whenever 64 are
+// queued, one pass measures 64 with every lane (p's bytes from the ring) and
+// keeps the best per walk in its result slot by atomicMax on length << 15 |
+// (0x7FFF - distance): the longest, then the nearest -- the walk's own
+// order, newest first, kept the first of equal length.  The walks then read
+// their slots back and tighten their filters; until then a walk filters
+// with an older best, which only lets through more candidates (measured, and
+// never longer than the best).  Lengths enter the key clamped at nice_len
+// (the walk stopped at the first such candidate): the winner's own length
+// is measured again at the end.  The streams are the ones of measuring at
+// once.
+struct MqState {
+  uint32_t head, tail;  // wave-uniform: entries [head, tail) of the ring are queued
+  uint32_t pbase, koff, pml;
+};
+__device__ __forceinline__ uint32_t mq_key(uint32_t len, uint32_t dist) { return (len << 15) | (0x7FFFu - dist); }
+
+__device__ __forceinline__ void mq_push_impl(MatchShared *s, MqState &m, bool c, uint32_t q, uint32_t slot) {
+  const uint64_t b = __ballot(c);
+  if (b) {
+    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+    if (c) s->mq[threadIdx.x >> 6][(m.tail + below) & 255] = q | (slot << 18);
+    m.tail += (uint32_t)__popcll(b);
+  }
+}
+#endif
 
 // one hop of two walks: every LDS load of both hops is issued before any is
 // used (the walks are latency-bound pointer chases), then the checks.  Per
@@ -892,9 +937,127 @@ __device__ __forceinline__ void walk_pair_step(Walk &a, Walk &b, const MatchShar
   b.link = lb;
   a.active = ha && la != 0 && step + 1 < a.max_hops;
   b.active = hb && lb != 0 && step + 1 < b.max_hops;
+#if defined(ZT_DF_X_EXT0)
+  // (measurement build: candidates measured at the first hop only -- wrong
+  // streams; the time without the later, divergent measurement passes)
+  if (ca && step == 0) walk_extend(a, s, P, qa);
+  if (cb && step == 0) walk_extend(b, s, P, qb);
+#else
   if (ca) walk_extend(a, s, P, qa);
   if (cb) walk_extend(b, s, P, qb);
+#endif
 }
+
+#ifdef ZT_DF_MQ
+// walk_pair_step with the candidates queued (above) instead of measured
+__device__ __forceinline__ void walk_pair_hop_mq(Walk &a, Walk &b, const MatchShared *s, int step, MqState &m) {
+  const uint32_t qa = a.q - a.link;
+  const uint32_t qb = b.q - b.link;
+  const bool ha = a.active && a.p - qa <= (uint32_t)DF_MAXDIST;
+  const bool hb = b.active && b.p - qb <= (uint32_t)DF_MAXDIST;
+  const uint32_t la = s->prev[ridx(qa)], lb = s->prev[ridx(qb)];
+  const uint32_t oa = ld32(s, qa + a.o), ob = ld32(s, qb + b.o);
+  a.q = qa;
+  b.q = qb;
+#ifdef ZT_DF_COUNT
+  if ((threadIdx.x & 63) == 0) atomicAdd(&g_df_count[0], 1ull);
+  atomicAdd(&g_df_count[1], (unsigned long long)(ha ? 1 : 0) + (hb ? 1 : 0));
+#endif
+  const bool ca = ha & (((oa ^ a.pw) & a.omask) == 0);
+  const bool cb = hb & (((ob ^ b.pw) & b.omask) == 0);
+  a.link = la;
+  b.link = lb;
+  a.active = ha && la != 0 && step + 1 < a.max_hops;
+  b.active = hb && lb != 0 && step + 1 < b.max_hops;
+  MatchShared *sw = const_cast<MatchShared *>(s);  // (the queue is the wave's own)
+  mq_push_impl(sw, m, ca, qa, 2 * (threadIdx.x & 63));
+  mq_push_impl(sw, m, cb, qb, 2 * (threadIdx.x & 63) + 1);
+}
+
+// bytes q.. against p.. from byte `len` on (16 per round) up to max_len
+__device__ __forceinline__ uint32_t mq_measure(const MatchShared *s, uint32_t q, uint32_t p, uint32_t max_len) {
+  uint32_t qw[4], pw[4];
+  ld_run<4>(s, q, qw);
+  ld_run<4>(s, p, pw);
+  uint32_t len = eq_len16(qw[0] ^ pw[0], qw[1] ^ pw[1], qw[2] ^ pw[2], qw[3] ^ pw[3]);
+  bool more = len == 16;
+  while (more && len < max_len) {
+    uint32_t qx[4], px[4];
+    ld_run<4>(s, q + len, qx);
+    ld_run<4>(s, p + len, px);
+    const uint32_t l = eq_len16(qx[0] ^ px[0], qx[1] ^ px[1], qx[2] ^ px[2], qx[3] ^ px[3]);
+    len += l;
+    more = l == 16;
+  }
+  return len < max_len ? len : max_len;
+}
+
+// one pass: the next min(64, queued) candidates, one per lane
+__device__ __forceinline__ void mq_process(const MatchShared *s, const DeflateParams &P, MqState &m) {
+  MatchShared *sw = const_cast<MatchShared *>(s);
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t n = (m.tail - m.head) < 64u ? (m.tail - m.head) : 64u;
+  if (lane < n) {
+    const uint32_t e = s->mq[wv][(m.head + lane) & 255];
+    const uint32_t q = e & 0x3FFFFu, slot = e >> 18;
+    const uint32_t p = m.pbase + 4 * (slot >> 1) + m.koff + 2 * (slot & 1);
+    const uint32_t ml = p < m.pml ? ((m.pml - p) < 258u ? (m.pml - p) : 258u) : 0u;
+    const uint32_t len = mq_measure(s, q, p, ml);
+    const uint32_t lk = len < (uint32_t)P.nice_len ? len : (uint32_t)P.nice_len;
+    if (len >= 3) atomicMax(&sw->mr[wv][slot], mq_key(lk, p - q));
+  }
+  m.head += n;
+}
+
+// the walk reads its result slot back (branch-free, as the measurement's own update)
+__device__ __forceinline__ void mq_poll(Walk &w, const MatchShared *s, const DeflateParams &P, uint32_t slot,
+                                        bool &from_q) {
+  const uint32_t k = s->mr[threadIdx.x >> 6][slot];
+  const uint32_t len = k >> 15;
+  const bool upd = len > w.best_len;
+  const bool stop = upd && ((int)len >= P.nice_len || len >= w.max_len);
+  const bool newo = upd && !stop && len >= 4;
+  w.best_len = upd ? len : w.best_len;
+  w.best_dist = upd ? 0x7FFFu - (k & 0x7FFFu) : w.best_dist;
+  from_q = from_q || upd;
+  w.active = w.active && !stop;
+  w.o = newo ? len - 3 : w.o;
+  w.omask = newo ? 0xFFFFFFFFu : w.omask;
+  const uint32_t npw = ld32(s, w.p + w.o);
+  w.pw = newo ? npw : w.pw;
+}
+
+// one pair loop of search_quad with queued measurement: the walks' slots
+// start at their carried match with the largest distance field, so that no
+// candidate of equal length replaces it (as the walk's strict > keeps it)
+__device__ __forceinline__ void mq_pair_loop(Walk &wa, Walk &wb, const MatchShared *s, const DeflateParams &P,
+                                             MqState &m) {
+  MatchShared *sw = const_cast<MatchShared *>(s);
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  sw->mr[wv][2 * lane] = wa.best_len >= 3 ? (wa.best_len << 15) | 0x7FFFu : 0u;
+  sw->mr[wv][2 * lane + 1] = wb.best_len >= 3 ? (wb.best_len << 15) | 0x7FFFu : 0u;
+  m.head = m.tail = 0;
+  bool fa = false, fb = false;
+  // (a wave-uniform loop: the passes need every lane, so no lane leaves
+  // before the last walk of the wave ends; an inactive walk's hops push nothing)
+  for (int step = 0; __ballot(wa.active || wb.active) != 0; ++step) {
+    walk_pair_hop_mq(wa, wb, s, step, m);
+    if (m.tail - m.head >= 64u) {
+      do {
+        mq_process(s, P, m);
+      } while (m.tail - m.head >= 64u);
+      mq_poll(wa, s, P, 2 * lane, fa);
+      mq_poll(wb, s, P, 2 * lane + 1, fb);
+    }
+  }
+  while (m.tail != m.head) mq_process(s, P, m);
+  mq_poll(wa, s, P, 2 * lane, fa);
+  mq_poll(wb, s, P, 2 * lane + 1, fb);
+  // a length clamped at nice_len: the winner's own length
+  if (fa && (int)wa.best_len >= P.nice_len) wa.best_len = mq_measure(s, wa.p - wa.best_dist, wa.p, wa.max_len);
+  if (fb && (int)wb.best_len >= P.nice_len) wb.best_len = mq_measure(s, wb.p - wb.best_dist, wb.p, wb.max_len);
+}
+#endif
 
 // finish position pb + K when the chain found nothing of the key's length:
 // the near probes, then the newest earlier position with the same 4 bytes
@@ -940,7 +1103,20 @@ __device__ __forceinline__ uint32_t walk_finish(const Walk &w, const MatchShared
 // matches end at pml (>= p1)
 __device__ void search_quad(const MatchShared *s, const DeflateParams &P, uint32_t pb, uint32_t p0, uint32_t p1,
                             uint32_t pml, uint32_t lim4, Key key, uint32_t *res_out) {
+#if defined(ZT_DF_MQ) && !defined(ZT_DF_HEAD16)
+#error "ZT_DF_MQ needs the LDS that ZT_DF_HEAD16 frees"
+#endif
+#ifdef ZT_DF_MQ
+  // (every lane stays: the queue's passes need the whole wave; lanes past
+  // the sub-chunk walk nothing and store nothing)
+  const bool valid = pb < p1;
+  if (!valid) pml = 0;
+  MqState m;
+  m.pbase = pb - 4 * (threadIdx.x & 63);
+  m.pml = __builtin_amdgcn_readfirstlane(pml);
+#else
   if (pb >= p1) return;
+#endif
   // bytes [pb - 16, pb + 20) (pb is a multiple of 4; before rel 0 the words
   // are never used: near distances stay <= p)
   uint32_t w[9];
@@ -953,7 +1129,12 @@ __device__ void search_quad(const MatchShared *s, const DeflateParams &P, uint32
   Walk wa, wb;
   walk_init(wa, s, P, pb, pml, win32<16>(w), win32<20>(w), win32<24>(w), win32<28>(w), 0, 0);
   walk_init(wb, s, P, pb + 2, pml, win32<18>(w), win32<22>(w), win32<26>(w), win32<30>(w), 0, 0);
+#ifdef ZT_DF_MQ
+  m.koff = 0;
+  mq_pair_loop(wa, wb, s, P, m);
+#else
   for (int step = 0; wa.active || wb.active; ++step) walk_pair_step(wa, wb, s, P, step);
+#endif
   out[0] = walk_finish<0>(wa, s, P, w, nr0, lim4, c0l, c0d);
   out[2] = walk_finish<2>(wb, s, P, w, nr2, lim4, c2l, c2d);
 #ifdef ZT_DF_NOCARRY  // experiment: positions 1 and 3 start without the carried match
@@ -961,7 +1142,12 @@ __device__ void search_quad(const MatchShared *s, const DeflateParams &P, uint32
 #endif
   walk_init(wa, s, P, pb + 1, pml, win32<17>(w), win32<21>(w), win32<25>(w), win32<29>(w), c0l, c0d);
   walk_init(wb, s, P, pb + 3, pml, win32<19>(w), win32<23>(w), win32<27>(w), win32<31>(w), c2l, c2d);
+#ifdef ZT_DF_MQ
+  m.koff = 1;
+  mq_pair_loop(wa, wb, s, P, m);
+#else
   for (int step = 0; wa.active || wb.active; ++step) walk_pair_step(wa, wb, s, P, step);
+#endif
   out[1] = walk_finish<1>(wa, s, P, w, nr1, lim4, cl, cd);
   out[3] = walk_finish<3>(wb, s, P, w, nr3, lim4, cl, cd);
   // the positions' own bytes (res_pack)
@@ -969,6 +1155,9 @@ __device__ void search_quad(const MatchShared *s, const DeflateParams &P, uint32
   out[1] |= win32<17>(w) << 24;
   out[2] |= win32<18>(w) << 24;
   out[3] |= win32<19>(w) << 24;
+#ifdef ZT_DF_MQ
+  if (!valid) return;
+#endif
   if (pb + 4 <= p1) {
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     u32x4 v = {out[0], out[1], out[2], out[3]};
@@ -1818,6 +2007,23 @@ __global__ __launch_bounds__(64, ZT_OP_MINW) void optparse_kernel(DeflateParams 
               {
                 const uint32_t kl = ((uint32_t)(dc + 0x8000 + c_far) << 9) | (Lc & 511);
                 key = (L > 10 && kl < key) ? kl : key;
+              }
+#elif defined(ZT_OP_SAT)
+              // a cut length past the match is priced out by (l - L, clamped
+              // at 0) << 25 -- keys stay below 2^25 -- instead of a compare
+              // and a select on VCC (each select waited on its compare)
+#pragma unroll
+              for (uint32_t l = 3; l < OP_SHORT; l += 2) {
+                uint32_t da, db;
+                asm("v_sub_u32_e64 %0, %1, %2 clamp" : "=v"(da) : "i"(l), "v"(L));
+                asm("v_sub_u32_e64 %0, %1, %2 clamp" : "=v"(db) : "i"(l + 1), "v"(L));
+                const uint32_t ka = (da << 25) + (base9 + cr9[l] + lk[l]);
+                const uint32_t kb = (db << 25) + (base9 + cr9[l + 1] + lk[l + 1]);
+                key = op_min3(key, ka, kb);
+              }
+              {
+                const uint32_t kl = ((uint32_t)(dc + 0x8000 + c_far) << 9) | (Lc & 511);
+                key = (L > OP_SHORT && kl < key) ? kl : key;
               }
 #else
 #pragma unroll
