@@ -222,6 +222,9 @@ def api_roundtrip(d_in, n, level, zt):
     iopts = zt.InflateOpts(1, 0x8000, 0)
     back = ctypes.POINTER(ctypes.c_uint8)()
     blen, ip = ctypes.c_size_t(), ctypes.c_size_t()
+    zt._check(zt.lib.zt_inflate_raw(out, olen.value, 0, ctypes.byref(iopts), ctypes.byref(back), ctypes.byref(blen),
+                                    ctypes.byref(ip)))  # warm (scratch and staging allocated once, as for deflate)
+    zt.lib.zt_free(back)
     t0 = time.perf_counter()
     zt._check(zt.lib.zt_inflate_raw(out, olen.value, 0, ctypes.byref(iopts), ctypes.byref(back), ctypes.byref(blen),
                                     ctypes.byref(ip)))

@@ -465,10 +465,6 @@ struct MatchShared {
   uint32_t head4[DF_H4SIZE];        // newest position (rel) per 4-byte-key bucket
   uint16_t link4[DF_SUB];           // position p of the sub-chunk: distance to the newest earlier
                                     // position of its 4-byte-key bucket (0 = none), at p % DF_SUB
-#ifdef ZT_DF_MQ
-  uint32_t mq[DF_THREADS / 64][256];  // per wave: candidates to measure (q | walk slot << 18), a ring
-  uint32_t mr[DF_THREADS / 64][128];  // per wave and walk slot: best (length << 15 | 0x7FFF - distance)
-#endif
   uint32_t dummy[4];                // exchange / link targets of lanes past the end (branch-free chain_link)
   uint32_t linked;                  // positions below are linked (chain_link -> searching waves)
   uint32_t linked4;                 // positions below have their 4-byte links
@@ -876,37 +872,6 @@ __device__ __forceinline__ void walk_extend(Walk &w, const MatchShared *s, const
 }
 
 
-#ifdef ZT_DF_MQ
-// Candidate measurement through a per-wave queue.  A hop's candidate (it
-// passed the filter) is appended to the wave's queue instead of being
-// measured at once -- at once, the wave ran the measurement whenever any of
-// its 128 walks had one: 1.5 passes per pair step with 4.7 lanes each on
-// text, about three times the VALU of the hops themselves.  Whenever 64 are
-// queued, one pass measures 64 with every lane (p's bytes from the ring) and
-// keeps the best per walk in its result slot by atomicMax on length << 15 |
-// (0x7FFF - distance): the longest, then the nearest -- the walk's own
-// order, newest first, kept the first of equal length.  The walks then read
-// their slots back and tighten their filters; until then a walk filters
-// with an older best, which only lets through more candidates (measured, and
-// never longer than the best).  Lengths enter the key clamped at nice_len
-// (the walk stopped at the first such candidate): the winner's own length
-// is measured again at the end.  The streams are the ones of measuring at
-// once.
-struct MqState {
-  uint32_t head, tail;  // wave-uniform: entries [head, tail) of the ring are queued
-  uint32_t pbase, koff, pml;
-};
-__device__ __forceinline__ uint32_t mq_key(uint32_t len, uint32_t dist) { return (len << 15) | (0x7FFFu - dist); }
-
-__device__ __forceinline__ void mq_push_impl(MatchShared *s, MqState &m, bool c, uint32_t q, uint32_t slot) {
-  const uint64_t b = __ballot(c);
-  if (b) {
-    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
-    if (c) s->mq[threadIdx.x >> 6][(m.tail + below) & 255] = q | (slot << 18);
-    m.tail += (uint32_t)__popcll(b);
-  }
-}
-#endif
 
 // one hop of two walks: every LDS load of both hops is issued before any is
 // used (the walks are latency-bound pointer chases), then the checks.  Per
@@ -948,116 +913,6 @@ __device__ __forceinline__ void walk_pair_step(Walk &a, Walk &b, const MatchShar
 #endif
 }
 
-#ifdef ZT_DF_MQ
-// walk_pair_step with the candidates queued (above) instead of measured
-__device__ __forceinline__ void walk_pair_hop_mq(Walk &a, Walk &b, const MatchShared *s, int step, MqState &m) {
-  const uint32_t qa = a.q - a.link;
-  const uint32_t qb = b.q - b.link;
-  const bool ha = a.active && a.p - qa <= (uint32_t)DF_MAXDIST;
-  const bool hb = b.active && b.p - qb <= (uint32_t)DF_MAXDIST;
-  const uint32_t la = s->prev[ridx(qa)], lb = s->prev[ridx(qb)];
-  const uint32_t oa = ld32(s, qa + a.o), ob = ld32(s, qb + b.o);
-  a.q = qa;
-  b.q = qb;
-#ifdef ZT_DF_COUNT
-  if ((threadIdx.x & 63) == 0) atomicAdd(&g_df_count[0], 1ull);
-  atomicAdd(&g_df_count[1], (unsigned long long)(ha ? 1 : 0) + (hb ? 1 : 0));
-#endif
-  const bool ca = ha & (((oa ^ a.pw) & a.omask) == 0);
-  const bool cb = hb & (((ob ^ b.pw) & b.omask) == 0);
-  a.link = la;
-  b.link = lb;
-  a.active = ha && la != 0 && step + 1 < a.max_hops;
-  b.active = hb && lb != 0 && step + 1 < b.max_hops;
-  MatchShared *sw = const_cast<MatchShared *>(s);  // (the queue is the wave's own)
-  mq_push_impl(sw, m, ca, qa, 2 * (threadIdx.x & 63));
-  mq_push_impl(sw, m, cb, qb, 2 * (threadIdx.x & 63) + 1);
-}
-
-// bytes q.. against p.. from byte `len` on (16 per round) up to max_len
-__device__ __forceinline__ uint32_t mq_measure(const MatchShared *s, uint32_t q, uint32_t p, uint32_t max_len) {
-  uint32_t qw[4], pw[4];
-  ld_run<4>(s, q, qw);
-  ld_run<4>(s, p, pw);
-  uint32_t len = eq_len16(qw[0] ^ pw[0], qw[1] ^ pw[1], qw[2] ^ pw[2], qw[3] ^ pw[3]);
-  bool more = len == 16;
-  while (more && len < max_len) {
-    uint32_t qx[4], px[4];
-    ld_run<4>(s, q + len, qx);
-    ld_run<4>(s, p + len, px);
-    const uint32_t l = eq_len16(qx[0] ^ px[0], qx[1] ^ px[1], qx[2] ^ px[2], qx[3] ^ px[3]);
-    len += l;
-    more = l == 16;
-  }
-  return len < max_len ? len : max_len;
-}
-
-// one pass: the next min(64, queued) candidates, one per lane
-__device__ __forceinline__ void mq_process(const MatchShared *s, const DeflateParams &P, MqState &m) {
-  MatchShared *sw = const_cast<MatchShared *>(s);
-  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const uint32_t n = (m.tail - m.head) < 64u ? (m.tail - m.head) : 64u;
-  if (lane < n) {
-    const uint32_t e = s->mq[wv][(m.head + lane) & 255];
-    const uint32_t q = e & 0x3FFFFu, slot = e >> 18;
-    const uint32_t p = m.pbase + 4 * (slot >> 1) + m.koff + 2 * (slot & 1);
-    const uint32_t ml = p < m.pml ? ((m.pml - p) < 258u ? (m.pml - p) : 258u) : 0u;
-    const uint32_t len = mq_measure(s, q, p, ml);
-    const uint32_t lk = len < (uint32_t)P.nice_len ? len : (uint32_t)P.nice_len;
-    if (len >= 3) atomicMax(&sw->mr[wv][slot], mq_key(lk, p - q));
-  }
-  m.head += n;
-}
-
-// the walk reads its result slot back (branch-free, as the measurement's own update)
-__device__ __forceinline__ void mq_poll(Walk &w, const MatchShared *s, const DeflateParams &P, uint32_t slot,
-                                        bool &from_q) {
-  const uint32_t k = s->mr[threadIdx.x >> 6][slot];
-  const uint32_t len = k >> 15;
-  const bool upd = len > w.best_len;
-  const bool stop = upd && ((int)len >= P.nice_len || len >= w.max_len);
-  const bool newo = upd && !stop && len >= 4;
-  w.best_len = upd ? len : w.best_len;
-  w.best_dist = upd ? 0x7FFFu - (k & 0x7FFFu) : w.best_dist;
-  from_q = from_q || upd;
-  w.active = w.active && !stop;
-  w.o = newo ? len - 3 : w.o;
-  w.omask = newo ? 0xFFFFFFFFu : w.omask;
-  const uint32_t npw = ld32(s, w.p + w.o);
-  w.pw = newo ? npw : w.pw;
-}
-
-// one pair loop of search_quad with queued measurement: the walks' slots
-// start at their carried match with the largest distance field, so that no
-// candidate of equal length replaces it (as the walk's strict > keeps it)
-__device__ __forceinline__ void mq_pair_loop(Walk &wa, Walk &wb, const MatchShared *s, const DeflateParams &P,
-                                             MqState &m) {
-  MatchShared *sw = const_cast<MatchShared *>(s);
-  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  sw->mr[wv][2 * lane] = wa.best_len >= 3 ? (wa.best_len << 15) | 0x7FFFu : 0u;
-  sw->mr[wv][2 * lane + 1] = wb.best_len >= 3 ? (wb.best_len << 15) | 0x7FFFu : 0u;
-  m.head = m.tail = 0;
-  bool fa = false, fb = false;
-  // (a wave-uniform loop: the passes need every lane, so no lane leaves
-  // before the last walk of the wave ends; an inactive walk's hops push nothing)
-  for (int step = 0; __ballot(wa.active || wb.active) != 0; ++step) {
-    walk_pair_hop_mq(wa, wb, s, step, m);
-    if (m.tail - m.head >= 64u) {
-      do {
-        mq_process(s, P, m);
-      } while (m.tail - m.head >= 64u);
-      mq_poll(wa, s, P, 2 * lane, fa);
-      mq_poll(wb, s, P, 2 * lane + 1, fb);
-    }
-  }
-  while (m.tail != m.head) mq_process(s, P, m);
-  mq_poll(wa, s, P, 2 * lane, fa);
-  mq_poll(wb, s, P, 2 * lane + 1, fb);
-  // a length clamped at nice_len: the winner's own length
-  if (fa && (int)wa.best_len >= P.nice_len) wa.best_len = mq_measure(s, wa.p - wa.best_dist, wa.p, wa.max_len);
-  if (fb && (int)wb.best_len >= P.nice_len) wb.best_len = mq_measure(s, wb.p - wb.best_dist, wb.p, wb.max_len);
-}
-#endif
 
 // finish position pb + K when the chain found nothing of the key's length:
 // the near probes, then the newest earlier position with the same 4 bytes
@@ -1103,20 +958,7 @@ __device__ __forceinline__ uint32_t walk_finish(const Walk &w, const MatchShared
 // matches end at pml (>= p1)
 __device__ void search_quad(const MatchShared *s, const DeflateParams &P, uint32_t pb, uint32_t p0, uint32_t p1,
                             uint32_t pml, uint32_t lim4, Key key, uint32_t *res_out) {
-#if defined(ZT_DF_MQ) && !defined(ZT_DF_HEAD16)
-#error "ZT_DF_MQ needs the LDS that ZT_DF_HEAD16 frees"
-#endif
-#ifdef ZT_DF_MQ
-  // (every lane stays: the queue's passes need the whole wave; lanes past
-  // the sub-chunk walk nothing and store nothing)
-  const bool valid = pb < p1;
-  if (!valid) pml = 0;
-  MqState m;
-  m.pbase = pb - 4 * (threadIdx.x & 63);
-  m.pml = __builtin_amdgcn_readfirstlane(pml);
-#else
   if (pb >= p1) return;
-#endif
   // bytes [pb - 16, pb + 20) (pb is a multiple of 4; before rel 0 the words
   // are never used: near distances stay <= p)
   uint32_t w[9];
@@ -1129,12 +971,7 @@ __device__ void search_quad(const MatchShared *s, const DeflateParams &P, uint32
   Walk wa, wb;
   walk_init(wa, s, P, pb, pml, win32<16>(w), win32<20>(w), win32<24>(w), win32<28>(w), 0, 0);
   walk_init(wb, s, P, pb + 2, pml, win32<18>(w), win32<22>(w), win32<26>(w), win32<30>(w), 0, 0);
-#ifdef ZT_DF_MQ
-  m.koff = 0;
-  mq_pair_loop(wa, wb, s, P, m);
-#else
   for (int step = 0; wa.active || wb.active; ++step) walk_pair_step(wa, wb, s, P, step);
-#endif
   out[0] = walk_finish<0>(wa, s, P, w, nr0, lim4, c0l, c0d);
   out[2] = walk_finish<2>(wb, s, P, w, nr2, lim4, c2l, c2d);
 #ifdef ZT_DF_NOCARRY  // experiment: positions 1 and 3 start without the carried match
@@ -1142,12 +979,7 @@ __device__ void search_quad(const MatchShared *s, const DeflateParams &P, uint32
 #endif
   walk_init(wa, s, P, pb + 1, pml, win32<17>(w), win32<21>(w), win32<25>(w), win32<29>(w), c0l, c0d);
   walk_init(wb, s, P, pb + 3, pml, win32<19>(w), win32<23>(w), win32<27>(w), win32<31>(w), c2l, c2d);
-#ifdef ZT_DF_MQ
-  m.koff = 1;
-  mq_pair_loop(wa, wb, s, P, m);
-#else
   for (int step = 0; wa.active || wb.active; ++step) walk_pair_step(wa, wb, s, P, step);
-#endif
   out[1] = walk_finish<1>(wa, s, P, w, nr1, lim4, cl, cd);
   out[3] = walk_finish<3>(wb, s, P, w, nr3, lim4, cl, cd);
   // the positions' own bytes (res_pack)
@@ -1155,9 +987,6 @@ __device__ void search_quad(const MatchShared *s, const DeflateParams &P, uint32
   out[1] |= win32<17>(w) << 24;
   out[2] |= win32<18>(w) << 24;
   out[3] |= win32<19>(w) << 24;
-#ifdef ZT_DF_MQ
-  if (!valid) return;
-#endif
   if (pb + 4 <= p1) {
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     u32x4 v = {out[0], out[1], out[2], out[3]};
@@ -1992,40 +1821,6 @@ __global__ __launch_bounds__(64, ZT_OP_MINW) void optparse_kernel(DeflateParams 
               // one add3 of pre-shifted terms (exact modulo 2^32: the
               // unshifted value is below 2^23)
               const uint32_t base9 = (uint32_t)(dc + 0x8000 - (int)C1) << 9;
-#ifdef ZT_OP_SPARSE
-              // every cut length up to 10, then the longest of each length
-              // symbol's range (the same length price: 12, 14, 16, 18, 22,
-              // 24), and the full match itself
-              constexpr uint32_t kCuts[14] = {3, 4, 5, 6, 7, 8, 9, 10, 12, 14, 16, 18, 22, 24};
-              static_assert(OP_SHORT == 24, "the sparse cut list ends at 24");
-#pragma unroll
-              for (int j = 0; j < 14; j += 2) {
-                const uint32_t l = kCuts[j], l2 = kCuts[j + 1];
-                const uint32_t ka = base9 + cr9[l] + lk[l], kb = base9 + cr9[l2] + lk[l2];
-                key = op_min3(key, l <= L ? ka : 0xFFFFFFFFu, l2 <= L ? kb : 0xFFFFFFFFu);
-              }
-              {
-                const uint32_t kl = ((uint32_t)(dc + 0x8000 + c_far) << 9) | (Lc & 511);
-                key = (L > 10 && kl < key) ? kl : key;
-              }
-#elif defined(ZT_OP_SAT)
-              // a cut length past the match is priced out by (l - L, clamped
-              // at 0) << 25 -- keys stay below 2^25 -- instead of a compare
-              // and a select on VCC (each select waited on its compare)
-#pragma unroll
-              for (uint32_t l = 3; l < OP_SHORT; l += 2) {
-                uint32_t da, db;
-                asm("v_sub_u32_e64 %0, %1, %2 clamp" : "=v"(da) : "i"(l), "v"(L));
-                asm("v_sub_u32_e64 %0, %1, %2 clamp" : "=v"(db) : "i"(l + 1), "v"(L));
-                const uint32_t ka = (da << 25) + (base9 + cr9[l] + lk[l]);
-                const uint32_t kb = (db << 25) + (base9 + cr9[l + 1] + lk[l + 1]);
-                key = op_min3(key, ka, kb);
-              }
-              {
-                const uint32_t kl = ((uint32_t)(dc + 0x8000 + c_far) << 9) | (Lc & 511);
-                key = (L > OP_SHORT && kl < key) ? kl : key;
-              }
-#else
 #pragma unroll
               for (uint32_t l = 3; l < OP_SHORT; l += 2) {
                 const uint32_t ka = base9 + cr9[l] + lk[l], kb = base9 + cr9[l + 1] + lk[l + 1];
@@ -2035,7 +1830,6 @@ __global__ __launch_bounds__(64, ZT_OP_MINW) void optparse_kernel(DeflateParams 
                 const uint32_t kl = ((uint32_t)(dc + 0x8000 + c_far) << 9) | (Lc & 511);
                 key = (L > OP_SHORT && kl < key) ? kl : key;
               }
-#endif
               const uint32_t choice = key & 511;
               const int best = (int)(key >> 9) - 0x8000;
               C1 += (uint32_t)best;

@@ -401,14 +401,17 @@ int inflate_dev_member(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t index
 // host bound -- returns 1 and the caller decodes the whole stream in one call
 // (tests/test_gpu_api_pipeline.py: identical output and end position).
 static constexpr size_t kInfPipeMin = 32u << 20;
-static constexpr size_t kInfPiece = 32u << 20;
+static constexpr size_t kInfPiece = 64u << 20;
 
 static int inflate_raw_pipelined(DeviceCtx *c, const uint8_t *in, size_t n, size_t index, uint8_t **out,
                                  size_t *out_len, size_t *end_ip) {
   static const uint8_t kMarker[10] = {0, 0, 0, 0xFF, 0xFF, 0, 0, 0, 0xFF, 0xFF};
   static const uint8_t kFinal[5] = {1, 0, 0, 0xFF, 0xFF};
   const size_t m = n - index;
-  const size_t piece = std::min(std::max(m / 16, (size_t)8 << 20), kInfPiece);
+  // tuning hook: ZT_INF_PIECES = pieces per stream (default 8; each piece's
+  // decode pays a few host round trips, so fewer, larger pieces)
+  static const int np_env = getenv("ZT_INF_PIECES") ? atoi(getenv("ZT_INF_PIECES")) : 0;
+  const size_t piece = std::min(std::max(m / (np_env > 1 ? np_env : 8), (size_t)8 << 20), kInfPiece);
   std::vector<size_t> cut{index};
   for (size_t t = index + piece; t + piece / 2 < n; t = cut.back() + piece) {
     const size_t lo = std::max(t, cut.back()) - 10, hi = std::min(n, t + (8u << 20));
