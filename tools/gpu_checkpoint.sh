@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round checkpoint on one GPU box: full GPU tests, smoke, the bench line,
-# rocprofv3 kernel stats of the bench and of C1 / C2 / C4 (the PMC HBM
-# traffic passes: tools/gpu_checkpoint_pmc.sh).
+# the 16-window ratio gate, rocprofv3 kernel stats of the bench and of C1 /
+# C2 / C4 (the PMC HBM traffic passes: tools/gpu_checkpoint_pmc.sh).
 #   usage: tools/gpu_checkpoint.sh TAG
 set -e
 TAG=${1:-ck}
@@ -14,6 +14,9 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 tail -1 gpurun_out/${TAG}_smoke.log
 timeout -k 10 600 python bench.py > gpurun_out/${TAG}_bench.log 2>&1
 tail -1 gpurun_out/${TAG}_bench.log
+# the 16-window ratio gate of this build (one gate log per checkpoint)
+timeout -k 10 300 python3 tools/ratio_gate.py > gpurun_out/${TAG}_gate.log 2>&1
+tail -1 gpurun_out/${TAG}_gate.log
 cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d $R/gpurun_out/${TAG}_prof -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-api > $R/gpurun_out/${TAG}_prof.log 2>&1
 cd $R
 cp gpurun_out/${TAG}_prof/run_kernel_stats.csv gpurun_out/${TAG}_kernel_stats.csv
