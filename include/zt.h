@@ -67,7 +67,11 @@ const char *zt_last_error_message(void);
 /* Library version string. */
 const char *zt_version(void);
 /* Free a buffer returned by the library (every output pointer, batch items
- * included; never free() them directly: batch items share allocations). */
+ * included; never free() them directly: batch items share allocations, and
+ * outputs of 8 MiB or more return to a bounded host output pool -- reused,
+ * registered with HIP, by the next output of a similar size; at most
+ * ZT_HOST_POOL_MB free MiB kept (default 4096, 0: no pool);
+ * zt_release_scratch drops them). */
 void zt_free(void *p);
 
 /* ---- checksums (host pointers) ------------------------------------------ */

@@ -130,3 +130,45 @@ def test_pipelined_inflate_zlib_stream(zt):
     s = co.compress(data) + co.flush()
     back, ip = zt.inflate_raw(s)
     assert ip == len(s) and back == data
+
+
+# ---- the host output pool (zt_api.cpp host_out): zt_free hands large outputs
+# back, the next output of a similar size reuses the buffer registered with
+# HIP, and copies to / from it go by DMA without staging.  The bench's host
+# round trip exactly: deflate output pointer straight into zt_inflate_raw.
+
+def test_host_output_pool_round_trips(zt):
+    import ctypes
+
+    import numpy as np
+    import torch
+
+    n = (96 << 20) + 4097
+    d_in = torch.empty(n, dtype=torch.uint8, device="cuda")
+    zt.synth_dev("mixed", 21, d_in.data_ptr(), n)
+    host = d_in.cpu().numpy()
+    src = host.ctypes.data_as(ctypes.c_void_p)
+    opts = zt.DeflateOpts(2, 0, 6)
+    iopts = zt.InflateOpts(1, 0x8000, 0)
+    first = None
+    held = []
+    for rep in range(4):
+        out = ctypes.POINTER(ctypes.c_uint8)()
+        olen = ctypes.c_size_t()
+        zt._check(zt.lib.zt_deflate_raw(src, n, ctypes.byref(opts), ctypes.byref(out), ctypes.byref(olen)))
+        s = ctypes.string_at(out, olen.value)
+        first = s if first is None else first
+        assert s == first  # the same stream from a fresh and from a reused (registered) buffer
+        back = ctypes.POINTER(ctypes.c_uint8)()
+        blen, ip = ctypes.c_size_t(), ctypes.c_size_t()
+        zt._check(zt.lib.zt_inflate_raw(out, olen.value, 0, ctypes.byref(iopts), ctypes.byref(back),
+                                        ctypes.byref(blen), ctypes.byref(ip)))
+        assert blen.value == n and ip.value == olen.value
+        assert np.array_equal(np.ctypeslib.as_array(back, shape=(n,)), host)
+        zt.lib.zt_free(out)
+        if rep == 1:
+            held.append(back)  # kept alive: the next outputs must not reuse it
+        else:
+            zt.lib.zt_free(back)
+    assert np.array_equal(np.ctypeslib.as_array(held[0], shape=(n,)), host)
+    zt.lib.zt_free(held[0])

@@ -507,9 +507,8 @@ __device__ __forceinline__ uint32_t ld8(const MatchShared *s, uint32_t rel) {
 // 4 bytes at any byte offset: an aligned dword pair and a byte align (an
 // unaligned ds_read_b32 is legal on gfx950 but measured 25-45 % slower here)
 __device__ __forceinline__ uint32_t ld32(const MatchShared *s, uint32_t rel) {
-  const uint32_t i = ridx(rel);
-  const uint2 v = ring_pair(s, i >> 2);
-  return __builtin_amdgcn_alignbyte(v.y, v.x, i);  // (v_alignbyte_b32 reads the shift's low 2 bits only)
+  const uint2 v = ring_pair(s, ridx(rel) >> 2);
+  return __builtin_amdgcn_alignbyte(v.y, v.x, rel);  // (v_alignbyte_b32 reads the shift's low 2 bits only)
 }
 // chain key at p: the first klen bytes (kmask: bytes 0-3, kmask2: bytes 4-7)
 struct Key {
@@ -755,7 +754,7 @@ struct Walk {
 // ring's end keeps up to 15 words contiguous): n + 1 dword loads, no wrap math
 template <int N>
 __device__ __forceinline__ void ld_run(const MatchShared *s, uint32_t rel, uint32_t (&o)[N]) {
-  const uint32_t i = ridx(rel), w = i >> 2, sh = i;  // (v_alignbyte_b32 reads the shift's low 2 bits only)
+  const uint32_t w = ridx(rel) >> 2, sh = rel;  // (v_alignbyte_b32 reads the shift's low 2 bits only)
   uint32_t d[N + 1];
   ring_dwords<N>(s, w, d);
 #pragma unroll

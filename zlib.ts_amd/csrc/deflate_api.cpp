@@ -120,7 +120,7 @@ static int deflate_raw_pipelined(DeviceCtx *c, const uint8_t *in, size_t n, int 
   ZT_TRY(scratch(c, 1, pb * np, &d_out));
   const size_t ss = deflate_scratch_bytes(c, piece);
   ZT_TRY(scratch(c, 3, ss, &d_scr));
-  uint8_t *h = host_out(pb * np);
+  uint8_t *h = host_out(pb * np, true);
   if (!h) return set_error(ZT_E_NOMEM, "host allocation failed");
   size_t total = 0;
   const int rc = pipeline_h2d_d2h(
@@ -165,7 +165,7 @@ int zt_deflate_raw(const uint8_t *in, size_t n, const zt_deflate_opts *opts, uin
   ZT_TRY(upload(c, d_in, in, n, c->stream));
   size_t len = 0;
   ZT_TRY(deflate_dev_run(c, (const uint8_t *)d_in, n, 0, 1, ct, lv, (uint8_t *)d_out, &len, d_scr, ss, c->stream));
-  uint8_t *h = host_out(len);
+  uint8_t *h = host_out(len, true);
   if (!h) return set_error(ZT_E_NOMEM, "host allocation failed");
   const int rc = download(c, h, d_out, len, c->stream);
   if (rc) {

@@ -429,7 +429,7 @@ static int inflate_raw_pipelined(DeviceCtx *c, const uint8_t *in, size_t n, size
   // outputs of up to 4x the input (the host bound below); past it: one call
   const size_t cap = std::max<size_t>(4 * m, 64u << 20);
   ZT_TRY(scratch(c, 22, cap, &d_out));
-  uint8_t *h = host_out(cap);  // (pages past the output are never touched)
+  uint8_t *h = host_out(cap, true);  // (pages past the output are never touched)
   if (!h) return set_error(ZT_E_NOMEM, "host allocation failed");
   auto d_piece = [&](size_t i) { return (uint8_t *)d_in + (cut[i] - index) + 64 * i; };
   size_t off = 0, eip_last = 0;
@@ -497,7 +497,7 @@ int zt_inflate_raw(const uint8_t *in, size_t n, size_t index, const zt_inflate_o
     if (seg >= 1) seg = inflate_general_dev(c, (const uint8_t *)d_in, n, index, &d_out, 0, &ol, &eip, c->stream);
     if (seg < 0) return seg;
     if (seg == 0) {
-      uint8_t *h = host_out(ol);
+      uint8_t *h = host_out(ol, true);
       if (!h) return set_error(ZT_E_NOMEM, "host allocation failed");
       const int rc = download(c, h, d_out, ol, c->stream);
       if (rc) {

@@ -246,114 +246,137 @@ __device__ __forceinline__ void expand_unit(const ResolveParams &P, ExpandShared
   sh.mark[lane] = 0;
   uint32_t seq = 0;
   uint32_t issued = 0;
-  uint32_t cur = 0, rem = 0;
   uint32_t op = 0;  // unit-relative output position
   bool bad = false;
-  while (cur < ntok) {
-    const uint32_t need = (cur >> 6) + 2 < nchunks ? (cur >> 6) + 2 : nchunks;
-    const uint32_t want = need + RS_AHEAD < nchunks ? need + RS_AHEAD : nchunks;
-    while (issued < want) {
-      __builtin_amdgcn_global_load_lds(tk + (uint64_t)issued * 64 + lane,
-                                       &sh.tok[(issued * 64) & (RS_TOK_RING - 1)], 4, 0, 0);
-      ++issued;
-    }
-    if (issued - need >= RS_AHEAD)
-      __builtin_amdgcn_s_waitcnt(0x0F70 | RS_AHEAD);  // vmcnt(RS_AHEAD)
-    else
-      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-    const uint32_t ti = cur + (uint32_t)lane;
-    const bool valid = ti < ntok;
-    const uint32_t t = sh.tok[ti & (RS_TOK_RING - 1)];
-    // a stored run at the cursor (tokenize_kernel: len << 16 with distance 0,
-    // then the payload's input offset in two tokens): its literal descriptors
-    // straight from the input, 8 bytes per lane in flight
-    const uint32_t t0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
-    if (RUNS && rem == 0 && (t0 >> 16) != 0 && (t0 & 0xFFFFu) == 0) {
-      const uint32_t rl = t0 >> 16;
-      const uint64_t src = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)t, 1) |
-                           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)t, 2) << 32);
-      const uint8_t *sp = P.in + src;
-      for (uint32_t i0 = 0; i0 < rl; i0 += 512) {
-        uint32_t b[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const uint32_t i = i0 + 64 * k + (uint32_t)lane;
-          b[k] = i < rl ? sp[i] : 0u;
-        }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const uint32_t i = i0 + 64 * k + (uint32_t)lane;
-          if (i < rl) desc[op + i] = (uint16_t)(0x8000u | b[k]);
-        }
-      }
-      // the copy step holding the run's end keeps its descriptors for the
-      // references of the tokens after it
-      const uint64_t pos = back + op, e = pos + rl;
-      const uint64_t ws_e = (e - 1) & ~uint64_t(CP_STEP - 1);
-      for (uint64_t x = (pos > ws_e ? pos : ws_e) + (uint64_t)lane; x < e; x += 64)
-        sh.cw[x - ws_e] = (uint16_t)(0x8000u | sp[x - pos]);
-      wave_sync();
-      op += rl;
-      cur += 3;
-      continue;
-    }
-    const uint32_t len = valid ? tok_len(t) : 0u;
-    const uint32_t S = wave_incl_scan(len);
-    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)S, 63) - rem;
-    // windows coincide with copy_kernel's 64-byte steps of the segment
+  // The scan of 64 token lengths is kept across windows: a window takes its
+  // bytes from the scan while the scan covers the whole window (a 64-token
+  // scan spans several windows but for literal-only stretches), and the
+  // tokens are re-read and re-scanned from the one holding the next byte
+  // only when it does not.  Scan coordinates: byte 0 = token cb's first byte.
+  uint32_t cb = 0;      // the scan's first token
+  uint32_t B = 0;       // scan coordinate of the next output byte
+  uint32_t j0 = 0;      // the scan's tokens that end at or before B
+  uint32_t T = 0;       // bytes the scan covers (up to its first stored run)
+  bool last = false;    // the scan holds the unit's last token (and no run)
+  bool scanned = false;
+  uint32_t t = 0, len = 0, S = 0;
+  bool valid = false;
+  while (cb + j0 < ntok) {
     const uint64_t pos = back + op;  // segment position of this window's first byte
+    // windows coincide with copy_kernel's 64-byte steps of the segment
     const uint32_t room = 64 - (uint32_t)(pos & 63);
-    uint32_t W = total < room ? total : room;
-    // a window ends where a stored run starts (the run is taken at the
-    // cursor); the run's two offset tokens after it are never scanned into one
-    const uint64_t runs = RUNS ? __ballot(valid && (t >> 16) != 0 && (t & 0xFFFFu) == 0) : 0ull;
-    if (RUNS && runs) {
-      const int fl = __ffsll((long long)runs) - 1;  // >= 1: a run at the cursor was taken above
-      const uint32_t rs = (uint32_t)__builtin_amdgcn_readlane((int)(S - len), fl) - rem;
-      W = rs < W ? rs : W;
+    if (!scanned || (T - B < room && !last)) {
+      // (re)scan from the token holding byte B; rem of its bytes are done
+      const uint32_t cur = cb + j0;
+      const uint32_t rem = j0 < 64 && scanned ? B - (uint32_t)__builtin_amdgcn_readlane((int)(S - len), j0) : 0u;
+      const uint32_t need = (cur >> 6) + 2 < nchunks ? (cur >> 6) + 2 : nchunks;
+      const uint32_t want = need + RS_AHEAD < nchunks ? need + RS_AHEAD : nchunks;
+      while (issued < want) {
+        __builtin_amdgcn_global_load_lds(tk + (uint64_t)issued * 64 + lane,
+                                         &sh.tok[(issued * 64) & (RS_TOK_RING - 1)], 4, 0, 0);
+        ++issued;
+      }
+      if (issued - need >= RS_AHEAD)
+        __builtin_amdgcn_s_waitcnt(0x0F70 | RS_AHEAD);  // vmcnt(RS_AHEAD)
+      else
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+      const uint32_t ti = cur + (uint32_t)lane;
+      valid = ti < ntok;
+      t = sh.tok[ti & (RS_TOK_RING - 1)];
+      // a stored run at the cursor (tokenize_kernel: len << 16 with distance 0,
+      // then the payload's input offset in two tokens): its literal descriptors
+      // straight from the input, 8 bytes per lane in flight
+      const uint32_t t0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
+      if (RUNS && rem == 0 && (t0 >> 16) != 0 && (t0 & 0xFFFFu) == 0) {
+        const uint32_t rl = t0 >> 16;
+        const uint64_t src = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)t, 1) |
+                             ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)t, 2) << 32);
+        const uint8_t *sp = P.in + src;
+        for (uint32_t i0 = 0; i0 < rl; i0 += 512) {
+          uint32_t b[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const uint32_t i = i0 + 64 * k + (uint32_t)lane;
+            b[k] = i < rl ? sp[i] : 0u;
+          }
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const uint32_t i = i0 + 64 * k + (uint32_t)lane;
+            if (i < rl) desc[op + i] = (uint16_t)(0x8000u | b[k]);
+          }
+        }
+        // the copy step holding the run's end keeps its descriptors for the
+        // references of the tokens after it
+        const uint64_t e = pos + rl;
+        const uint64_t ws_e = (e - 1) & ~uint64_t(CP_STEP - 1);
+        for (uint64_t x = (pos > ws_e ? pos : ws_e) + (uint64_t)lane; x < e; x += 64)
+          sh.cw[x - ws_e] = (uint16_t)(0x8000u | sp[x - pos]);
+        wave_sync();
+        op += rl;
+        cb = cur + 3;
+        j0 = 0;
+        B = 0;
+        scanned = false;
+        continue;
+      }
+      len = valid ? tok_len(t) : 0u;
+      S = wave_incl_scan(len);
+      T = (uint32_t)__builtin_amdgcn_readlane((int)S, 63);
+      last = cur + 64 >= ntok;
+      // the scan ends where a stored run starts (the run is taken at the
+      // cursor); the run's two offset tokens after it are never scanned into one
+      const uint64_t runs = RUNS ? __ballot(valid && (t >> 16) != 0 && (t & 0xFFFFu) == 0) : 0ull;
+      if (RUNS && runs) {
+        const int fl = __ffsll((long long)runs) - 1;  // >= 1: a run at the cursor was taken above
+        T = (uint32_t)__builtin_amdgcn_readlane((int)(S - len), fl);
+        last = false;
+      }
+      cb = cur;
+      B = rem;
+      j0 = 0;
+      scanned = true;
     }
+    const uint32_t W = T - B < room ? T - B : room;
     const uint64_t ws = pos & ~uint64_t(CP_STEP - 1);
     ++seq;
-    const int32_t p = (int32_t)S - (int32_t)rem;
+    // tokens that end inside the window mark the next token's start
+    const int32_t p = (int32_t)S - (int32_t)B;
     if (valid && p > 0 && p < 64) sh.mark[p] = seq;
     wave_sync();
     const uint64_t starts = __ballot(sh.mark[lane] == seq);
-    const uint32_t owner = __popcll(starts & (~0ull >> (63 - lane)));  // token of byte `lane`
+    const uint32_t owner = j0 + __popcll(starts & (~0ull >> (63 - lane)));  // token of byte `lane`
     const uint32_t tj = bperm(t, owner);
-    const uint32_t ej = bperm(S - len, owner);  // the token's start, relative to the cursor token
+    const uint32_t ej = bperm(S - len, owner);  // the token's start (scan coordinates)
     // descriptor: 0x8000 | byte (literal), 0xC000 | o (= byte ws + o, before
     // this unit), or ws - src - 1 (a byte before the copy step); references
     // into the step are followed here (earlier windows from LDS, this window
     // by pointer jumping over the lanes)
-    uint32_t dsc = 0x8000u;
-    int32_t ptr = -1;
-    uint32_t first = 0;  // step offset of the byte's direct source
-    if ((uint32_t)lane < W) {
-      if ((tj >> 16) == 0) {
-        dsc = 0x8000u | (tj & 0xFF);
-      } else {
-        const uint32_t dist = tj & 0xFFFF;
-        const uint32_t k = rem + (uint32_t)lane - ej;  // byte index inside the match
-        const uint32_t D = k < dist ? dist : dist * (1 + k / dist);
-        const uint64_t x = pos + lane;
-        if ((uint64_t)D > x && !behind_ok) {
-          bad = true;  // reaches behind the segment start
-        } else {
-          // (marker segments: a source before the segment start is a byte of
-          // the previous segment's last 32 KiB, D <= 32768 keeps it in the ring)
-          const int64_t src = (int64_t)x - (int64_t)D;
-          if (src < (int64_t)ws)
-            dsc = (uint32_t)((int64_t)ws - src - 1);
-          else if (src < (int64_t)back)
-            dsc = 0xC000u | (uint32_t)(src - (int64_t)ws);  // before this unit: copy_kernel resolves it
-          else if (src < (int64_t)pos)
-            dsc = safe_desc(sh.cw[src - (int64_t)ws], (uint32_t)(src - (int64_t)ws));  // an earlier window
-          else
-            ptr = (int32_t)(src - (int64_t)pos);
-          first = (uint32_t)(src - (int64_t)ws);
-        }
-      }
-    }
+    // Branch-free, in step-relative 32-bit offsets: the window lies inside
+    // one copy step (po + lane < CP_STEP) and a source is at most 32768 + 257
+    // bytes back.  k / dist in single precision: (k + 0.5) / dist is at
+    // least 0.5 / dist from an integer, far above v_rcp_f32's error at
+    // k < 258 (the quotient only matters when k >= dist, i.e. dist < 258).
+    const uint32_t po = (uint32_t)(pos - ws);
+    const uint32_t bo = back > ws ? (uint32_t)(back - ws) : 0u;
+    const bool near_start = pos < 65536u && !behind_ok;
+    const bool match = (uint32_t)lane < W && (tj >> 16) != 0;
+    const uint32_t dist = tj & 0xFFFF;
+    const uint32_t k = B + (uint32_t)lane - ej;  // byte index inside the match
+    const uint32_t kq = (uint32_t)(((float)k + 0.5f) * __builtin_amdgcn_rcpf((float)dist));  // k / dist
+    const uint32_t D = __umul24(dist, kq + 1u);
+    const bool b = match && near_start && D > (uint32_t)pos + (uint32_t)lane;  // reaches behind the segment start
+    bad = bad || b;
+    // (marker segments: a source before the segment start is a byte of the
+    // previous segment's last 32 KiB, D <= 32768 keeps it in the ring)
+    const int32_t so = (int32_t)(po + (uint32_t)lane) - (int32_t)D;  // source, relative to the step
+    const uint32_t cwv = sh.cw[so < 0 ? 0u : (uint32_t)so & (CP_STEP - 1)];  // (an earlier window's)
+    const uint32_t dm = so < 0 ? (uint32_t)(-so - 1)                         // before the copy step
+                        : so < (int32_t)bo ? (0xC000u | (uint32_t)so)          // before this unit: copy_kernel resolves it
+                                           : safe_desc(cwv, (uint32_t)so);
+    const bool m_ok = match && !b;
+    uint32_t dsc = m_ok ? dm : 0x8000u | (tj & 0xFF);  // (lanes past W: never read or written)
+    int32_t ptr = m_ok && so >= (int32_t)po ? so - (int32_t)po : -1;
+    const uint32_t first = (uint32_t)so;  // step offset of the byte's direct source
     const bool jumped = ptr >= 0;
     while (__ballot(ptr >= 0)) {
       const uint32_t q = ptr >= 0 ? (uint32_t)ptr : (uint32_t)lane;
@@ -371,15 +394,12 @@ __device__ __forceinline__ void expand_unit(const ResolveParams &P, ExpandShared
     if (jumped) dsc = safe_desc(dsc, first);
     if ((uint32_t)lane < W) {
       desc[op + lane] = (uint16_t)dsc;
-      sh.cw[pos - ws + lane] = (uint16_t)dsc;
+      sh.cw[po + lane] = (uint16_t)dsc;
     }
     wave_sync();
     op += W;
-    const uint64_t done = __ballot(valid && S <= rem + W);
-    const uint32_t kdone = (uint32_t)__popcll(done);
-    const uint32_t s_last = kdone ? (uint32_t)__builtin_amdgcn_readlane((int)S, kdone - 1) : 0u;
-    rem = rem + W - s_last;
-    cur += kdone;
+    B += W;
+    j0 = (uint32_t)__popcll(__ballot(valid && S <= B));
   }
   const bool any_bad = __ballot(bad) != 0;
   if (lane == 0) P.unit_status[u] = any_bad ? ZT_E_INVALID_DISTANCE : (op != cu.out_len ? ZT_E_INPUT_BROKEN : ZT_OK);
@@ -494,6 +514,22 @@ __device__ __forceinline__ uint32_t cp_byte(const CopyShared *sh, uint64_t op, u
   return lit ? (d & 0xFF) : rv;
 }
 
+// the two descriptors of a dword (low half first) -> their bytes in bits
+// 0-7 of lo / hi (bits 8-31 left unspecified).  A literal is selected by its
+// sign-extended bit 15 in one 3-input bit select (v_bitop3) instead of a
+// compare and a VCC select; the low half's ring index needs no extract
+// ((opm1 - x) mod 2^15 = (opm1 - d0) mod 2^15).  Only for steps with no
+// in-step reference.
+__device__ __forceinline__ void cp_pair(const CopyShared *sh, uint32_t opm1, uint32_t x, uint32_t &lo, uint32_t &hi) {
+  const uint32_t d1 = x >> 16;
+  const uint32_t r0 = sh->ring[(opm1 - x) & RING_MASK];
+  const uint32_t r1 = sh->ring[(opm1 - d1) & RING_MASK];
+  const uint32_t m0 = (uint32_t)__builtin_amdgcn_sbfe((int)x, 15, 1);  // ~0: a literal
+  const uint32_t m1 = (uint32_t)((int32_t)x >> 31);
+  lo = __builtin_amdgcn_bitop3_b32(m0, x, r0, 0xCA);  // m ? a : b, bitwise
+  hi = __builtin_amdgcn_bitop3_b32(m1, d1, r1, 0xCA);
+}
+
 #ifdef ZT_CP_TIME
 __device__ unsigned long long g_cp_time[8];  // debug: copy_kernel cycles per phase (lane 0 of each wave), [6] steps, [7] waves
 #define CP_T(v) v = __builtin_readcyclecounter()
@@ -539,18 +575,22 @@ __global__ __launch_bounds__(64) void copy_kernel(ResolveParams P) {
     CP_T(ct0);
     // every byte of a step is a literal or a ring byte before the step, so
     // all ring reads are issued before any write
+    // (an in-step reference 0xC000 | o is the only descriptor with bits 15
+    // and 14 both set: one AND with its own shift per dword finds any)
     uint32_t bw[CP_G];
-    bool in_step = false;
+    uint32_t refs = 0;
+    const uint32_t opm1 = (uint32_t)op - 1;
 #pragma unroll
     for (int g = 0; g < CP_G; ++g) {
-      int32_t o0, o1, o2, o3;
-      const uint32_t b0 = cp_byte(&sh, op, (uint32_t)dd[g] & 0xFFFF, o0);
-      const uint32_t b1 = cp_byte(&sh, op, (uint32_t)(dd[g] >> 16) & 0xFFFF, o1);
-      const uint32_t b2 = cp_byte(&sh, op, (uint32_t)(dd[g] >> 32) & 0xFFFF, o2);
-      const uint32_t b3 = cp_byte(&sh, op, (uint32_t)(dd[g] >> 48), o3);
-      bw[g] = b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
-      in_step = in_step || o0 >= 0 || o1 >= 0 || o2 >= 0 || o3 >= 0;
+      const uint32_t x0 = (uint32_t)dd[g], x1 = (uint32_t)(dd[g] >> 32);
+      refs |= (x0 & (x0 << 1)) | (x1 & (x1 << 1));
+      uint32_t b0, b1, b2, b3;
+      cp_pair(&sh, opm1, x0, b0, b1);
+      cp_pair(&sh, opm1, x1, b2, b3);
+      // bytes 0 of b0, b1 and of b2, b3 side by side, the pairs joined
+      bw[g] = __builtin_amdgcn_perm(b1, b0, 0x0C0C0400u) | (__builtin_amdgcn_perm(b3, b2, 0x0C0C0400u) << 16);
     }
+    const bool in_step = (refs & 0x80008000u) != 0;
     CP_T(ct2);
     if (__ballot(in_step) == 0) {
 #pragma unroll

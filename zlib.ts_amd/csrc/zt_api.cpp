@@ -133,15 +133,110 @@ int scratch(DeviceCtx *c, int slot, size_t bytes, void **ptr) {
   return ZT_OK;
 }
 
-uint8_t *host_out(size_t n) {
-  if (n < (8u << 20)) return (uint8_t *)malloc(n ? n : 1);
-  // large outputs: 2 MiB-aligned and backed by transparent huge pages where
-  // the kernel allows it -- 512x fewer first-touch faults while the
-  // download fills them (freed by zt_free = free)
+// The single-buffer calls' large host outputs (zt_deflate_raw /
+// zt_inflate_raw, >= 8 MiB) come from a bounded pool (a caching host
+// allocator): zt_free returns such a buffer to the pool -- registered with
+// HIP (hipHostRegister) on its first return, a one-time cost of that
+// zt_free (~25 ms per GiB, pages past the written output faulted in) -- and
+// the next output of a similar size reuses it, so downloads into it and
+// uploads from it (a stream handed back to zt_inflate_raw) go by DMA with no
+// pinned staging, host memcpy or page faults.  The free buffers the pool
+// keeps are bounded by ZT_HOST_POOL_MB (default 4096; 0: no pool, every
+// output freshly allocated); zt_release_scratch drops them.  Batch and
+// container outputs are not pooled (one-shot callers would pay the
+// registration for nothing).
+static uint8_t *host_alloc(size_t n) {
+  // 2 MiB-aligned and backed by transparent huge pages where the kernel
+  // allows it -- 512x fewer first-touch faults while the download fills them
   void *p = nullptr;
   if (posix_memalign(&p, 2u << 20, n)) return nullptr;
   (void)madvise(p, n, MADV_HUGEPAGE);
   return (uint8_t *)p;
+}
+
+struct PoolBuf {
+  uint8_t *p;
+  size_t cap;
+  bool used;
+  bool reg;      // registered with HIP
+  bool reg_bad;  // registration failed once: not tried again
+};
+static std::mutex g_pool_mu;
+static std::vector<PoolBuf> g_pool;
+
+static size_t pool_limit() {
+  static const size_t v = [] {
+    const char *e = getenv("ZT_HOST_POOL_MB");
+    return e ? (size_t)strtoull(e, nullptr, 10) << 20 : (size_t)4096 << 20;
+  }();
+  return v;
+}
+
+// free pool buffers beyond the bound, largest first (g_pool_mu held)
+static void pool_trim(size_t limit) {
+  for (;;) {
+    size_t free_bytes = 0, big = SIZE_MAX;
+    for (size_t i = 0; i < g_pool.size(); ++i)
+      if (!g_pool[i].used) {
+        free_bytes += g_pool[i].cap;
+        if (big == SIZE_MAX || g_pool[i].cap > g_pool[big].cap) big = i;
+      }
+    if (free_bytes <= limit || big == SIZE_MAX) return;
+    if (g_pool[big].reg) (void)hipHostUnregister(g_pool[big].p);
+    free(g_pool[big].p);
+    g_pool.erase(g_pool.begin() + (long)big);
+  }
+}
+
+uint8_t *host_out(size_t n, bool pool) {
+  if (n < (8u << 20)) return (uint8_t *)malloc(n ? n : 1);
+  if (!pool || !pool_limit()) return host_alloc(n);
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    size_t best = SIZE_MAX;
+    for (size_t i = 0; i < g_pool.size(); ++i) {
+      const PoolBuf &e = g_pool[i];
+      if (!e.used && e.cap >= n && e.cap / 2 <= n && (best == SIZE_MAX || e.cap < g_pool[best].cap)) best = i;
+    }
+    if (best != SIZE_MAX) {
+      g_pool[best].used = true;
+      return g_pool[best].p;
+    }
+  }
+  uint8_t *p = host_alloc(n);
+  if (!p) return nullptr;
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  g_pool.push_back(PoolBuf{p, n, true, false, false});
+  return p;
+}
+
+// a pool buffer back to the pool (false: p is not one)
+static bool pool_release(void *p) {
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  for (PoolBuf &e : g_pool)
+    if (e.p == p && e.used) {
+      e.used = false;
+      if (!e.reg && !e.reg_bad) {
+        e.reg = hipHostRegister(e.p, e.cap, hipHostRegisterPortable) == hipSuccess;
+        e.reg_bad = !e.reg;
+        if (!e.reg) (void)hipGetLastError();
+      }
+      pool_trim(pool_limit());
+      return true;
+    }
+  return false;
+}
+
+void host_release(void *p) {
+  if (!pool_release(p)) free(p);
+}
+
+bool host_direct(const void *p, size_t n) {
+  const uint8_t *q = static_cast<const uint8_t *>(p);
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  for (const PoolBuf &e : g_pool)
+    if (e.used && e.reg && q >= e.p && q + n <= e.p + e.cap) return true;
+  return false;
 }
 
 // Batch outputs share one host allocation (a slab, on huge pages when large):
@@ -172,7 +267,7 @@ bool slab_release(void *p) {
   --it;
   if ((uintptr_t)p >= it->first + it->second.size) return false;
   if (--it->second.refs == 0) {
-    free(reinterpret_cast<void *>(it->first));
+    host_release(reinterpret_cast<void *>(it->first));
     g_slabs.erase(it);
   }
   return true;
@@ -229,7 +324,7 @@ static int xfer_setup(DeviceCtx *c, uint8_t **buf) {
 }
 
 int upload(DeviceCtx *c, void *d_dst, const void *h_src, size_t n, hipStream_t s) {
-  if (n < (8u << 20)) {
+  if (n < (8u << 20) || host_direct(h_src, n)) {
     if (n) ZT_HIP(hipMemcpyAsync(d_dst, h_src, n, hipMemcpyHostToDevice, s));
     return ZT_OK;
   }
@@ -249,7 +344,7 @@ int upload(DeviceCtx *c, void *d_dst, const void *h_src, size_t n, hipStream_t s
 }
 
 int download(DeviceCtx *c, void *h_dst, const void *d_src, size_t n, hipStream_t s) {
-  if (n < (8u << 20)) {
+  if (n < (8u << 20) || host_direct(h_dst, n)) {
     if (n) ZT_HIP(hipMemcpyAsync(h_dst, d_src, n, hipMemcpyDeviceToHost, s));
     ZT_HIP(hipStreamSynchronize(s));
     return ZT_OK;
@@ -325,6 +420,9 @@ int pipeline_h2d_d2h(DeviceCtx *c, size_t np, const std::function<PipePiece(size
     size_t k = 0;  // chunks issued
     for (size_t i = 0; i < np && !failed(); ++i) {
       const PipePiece pc = input(i);
+      if (host_direct(pc.h_src, pc.n)) {  // (a registered pool buffer: DMA from it)
+        if (pc.n) ZT_HIP(hipMemcpyAsync(pc.d_dst, pc.h_src, pc.n, hipMemcpyHostToDevice, c->up));
+      } else
       for (size_t off = 0; off < pc.n; off += kXferChunk, ++k) {
         const size_t len = std::min(kXferChunk, pc.n - off);
         if (k >= 2) ZT_HIP(hipEventSynchronize(c->xfer_ev[k & 1]));
@@ -342,6 +440,7 @@ int pipeline_h2d_d2h(DeviceCtx *c, size_t np, const std::function<PipePiece(size
   };
   // stage 3: device -> pinned chunk (DMA on c->dn) -> host (host threads)
   size_t total = 0;
+  const bool direct = host_direct(out_base, out_cap);  // a registered pool buffer: DMA straight into it
   auto dn_stage = [&]() -> int {
     ZT_HIP(hipSetDevice(dev));
     size_t k = 0;
@@ -353,6 +452,11 @@ int pipeline_h2d_d2h(DeviceCtx *c, size_t np, const std::function<PipePiece(size
       }
       const size_t n = res_n[i];
       if (total + n > out_cap) return set_error(ZT_E_ARG, "pipeline output larger than its bound");
+      if (direct) {
+        if (n) ZT_HIP(hipMemcpyAsync(out_base + total, res[i], n, hipMemcpyDeviceToHost, c->dn));
+        total += n;
+        continue;
+      }
       // chunks of this piece: issue k + 1 before copying k out of its staging buffer
       const size_t nch = (n + kXferChunk - 1) / kXferChunk;
       auto issue = [&](size_t j) -> int {
@@ -372,6 +476,7 @@ int pipeline_h2d_d2h(DeviceCtx *c, size_t np, const std::function<PipePiece(size
       k += nch;
       total += n;
     }
+    if (direct) ZT_HIP(hipStreamSynchronize(c->dn));
     return ZT_OK;
   };
   std::thread tu([&] {
@@ -475,7 +580,7 @@ const char *zt_version(void) { return "zlib.ts_amd 0.1 (gfx950)"; }
 void zt_free(void *p) {
   if (!p) return;
   if (slab_release(p)) return;
-  free(p);
+  host_release(p);
 }
 
 int zt_dev_checksums(const void *d_in, size_t n, uint32_t crc_in, uint32_t adler_in, uint32_t *crc_out,
@@ -569,6 +674,8 @@ int zt_release_scratch(void) {
     c->h_pinned[k] = nullptr;
     c->pinned_size[k] = 0;
   }
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  pool_trim(0);  // the host output pool's free buffers
   return ZT_OK;
 }
 

@@ -84,8 +84,14 @@ int get_ctx(DeviceCtx **out);
 int scratch(DeviceCtx *c, int slot, size_t bytes, void **ptr);
 // Grow-only pinned host staging buffer `slot` (0 or 1) of at least `bytes`.
 int pinned(DeviceCtx *c, size_t bytes, void **ptr, int slot = 0);
-// Host output buffer the caller frees with zt_free (large ones on huge pages).
-uint8_t *host_out(size_t n);
+// Host output buffer the caller frees with zt_free (large ones on huge pages;
+// pool = true: from the bounded host output pool, zt_api.cpp); host_release
+// is zt_free's second half (back to the pool, or free).  host_direct: [p,
+// p + n) lies in a pool buffer registered with HIP, so copies to / from it go
+// by DMA without staging.
+uint8_t *host_out(size_t n, bool pool = false);
+void host_release(void *p);
+bool host_direct(const void *p, size_t n);
 // One host allocation for `items` batch outputs (pointers inside it, each
 // released by zt_free; reserve >= 1 byte per item so every pointer is
 // distinct).  slab_release: true when p lay in a slab (and was released).
