@@ -204,7 +204,9 @@ def api_roundtrip(d_in, n, level, zt):
     """The round trip through the host-buffer entry points (what a Node
     caller of RawDeflate / RawInflate runs): zt_deflate_raw of a host copy of
     the corpus, then zt_inflate_raw of the host stream, each C call timed
-    (PCIe transfers, pinning and host output allocation included)."""
+    after one warm-up call of its own (PCIe transfers included; the outputs
+    come from the library's host output pool, which the warm-up's zt_free
+    filled -- a steady-state caller's case, zt_api.cpp host_out)."""
     import ctypes
 
     import numpy as np
@@ -237,7 +239,9 @@ def api_roundtrip(d_in, n, level, zt):
     g = n / 2**30
     return {"deflate_GiBps": round(g / t_def, 3), "inflate_GiBps": round(g / t_inf, 3),
             "roundtrip_GiBps": round(g / (t_def + t_inf), 3),
-            "note": "zt_deflate_raw + zt_inflate_raw on pageable host buffers, PCIe and host allocation included"}
+            "note": "zt_deflate_raw of a pageable host copy, then zt_inflate_raw of its host stream, each after one "
+                    "warm-up call: PCIe included; outputs from the library's host output pool (zt_free of the warm-up "
+                    "outputs registered them, ZT_HOST_POOL_MB)"}
 
 
 # ---------------------------------------------------------------- ranks
