@@ -136,11 +136,12 @@ def pmc_traffic(kernel, n):
 
 
 def pmc_lds(kernel, n):
-    """The kernel's binding resource (SURVEY 8(d) honesty note: LZ77 match
-    finding is LDS-bound, not HBM-bound): the LDS array's busy fraction of
-    the kernel's CU-cycles and the bank-conflict share of those cycles, from
-    profiles/pmc_lds.json (tools/pmc_lds.py over a rocprofv3 SQ pass of this
-    workload) -- or None when it was measured on other kernel sources."""
+    """Where the kernel's cycles go beside HBM (SURVEY 8(d) honesty note: LZ77
+    match finding is bound on chip, not by HBM): the LDS array's busy fraction
+    of the kernel's CU-cycles and the bank-conflict share of those cycles,
+    and the SIMDs' VALU busy fraction, per launch, from profiles/pmc_lds.json
+    (tools/pmc_lds.py over a rocprofv3 SQ pass of this workload) -- or None
+    when it was measured on other kernel sources."""
     path = os.path.join(HERE, "profiles", "pmc_lds.json")
     try:
         with open(path) as f:
@@ -149,8 +150,12 @@ def pmc_lds(kernel, n):
         return None
     if d.get("kernel") != kernel or n != 1 << 30 or d.get("source_sha256") != source_digest():
         return None
-    return {"bound": "lds", "busy_frac": d["busy_frac"], "bank_conflict_frac": d["bank_conflict_frac"],
-            "source": "profiles/pmc_lds.json"}
+    out = {"busy_frac": d["busy_frac"], "bank_conflict_frac": d["bank_conflict_frac"]}
+    if d.get("valu_busy_frac") is not None:
+        out["valu_busy_frac"] = d["valu_busy_frac"]
+        out["wave_parked_frac"] = d.get("wave_parked_frac")
+    out["source"] = "profiles/pmc_lds.json"
+    return out
 
 
 def host_info():

@@ -15,9 +15,10 @@ timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE -f csv -d $R/gpurun_out/${TAG}_pm
 cd $R
 python3 tools/pmc_traffic.py profiles/pmc_traffic.json gpurun_out/${TAG}_pmcf gpurun_out/${TAG}_pmcq gpurun_out/${TAG}_pmcw > gpurun_out/${TAG}_pmc.txt && cp profiles/pmc_traffic.json gpurun_out/${TAG}_pmc_traffic.json
 grep -E 'match_kernel|tokenize|copy_kernel|checksum' gpurun_out/${TAG}_pmc.txt || true
-# the match kernel's LDS-array busy fraction (roofline.lds): an SQ pass + the kernel's average duration
+# the match kernel's LDS-array and VALU busy fractions (roofline.lds): an SQ pass (6 SQ counters) + the
+# kernel's average duration
 cd /tmp
-timeout -s KILL 180 rocprofv3 --pmc SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES SQ_WAVE_CYCLES -f csv -d $R/gpurun_out/${TAG}_pmcl -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-api > $R/gpurun_out/${TAG}_pmcl.log 2>&1
+timeout -s KILL 180 rocprofv3 --pmc SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_WAIT_ANY -f csv -d $R/gpurun_out/${TAG}_pmcl -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-api > $R/gpurun_out/${TAG}_pmcl.log 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $R/gpurun_out/${TAG}_pmcs -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-api > $R/gpurun_out/${TAG}_pmcs.log 2>&1
 cd $R
 python3 tools/pmc_lds.py profiles/pmc_lds.json gpurun_out/${TAG}_pmcl gpurun_out/${TAG}_pmcs/run_kernel_stats.csv > gpurun_out/${TAG}_pmc_lds.txt && cp profiles/pmc_lds.json gpurun_out/${TAG}_pmc_lds.json
