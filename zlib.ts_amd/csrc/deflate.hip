@@ -765,7 +765,7 @@ __device__ __forceinline__ void ld_run(const MatchShared *s, uint32_t rel, uint3
 // are bytes 0..15 of p
 __device__ __forceinline__ void walk_init(Walk &w, const MatchShared *s, const DeflateParams &P, uint32_t p, uint32_t p1,
                                           uint32_t cur, uint32_t cur2, uint32_t cur3, uint32_t cur4,
-                                          uint32_t carry_len, uint32_t carry_dist) {
+                                          uint32_t carry_len, uint32_t carry_dist, uint32_t link) {
   w.p = p;
   w.q = p;
   w.cur = cur;
@@ -796,7 +796,7 @@ __device__ __forceinline__ void walk_init(Walk &w, const MatchShared *s, const D
   w.link = 0;
   if (w.active) {
     if (w.best_len >= 4) w.pw = ld32(s, p + w.o);
-    w.link = s->prev[ridx(p)];
+    w.link = link;  // prev[ridx(p)], read by search_quad with its three neighbours
     w.active = w.link != 0;
   }
 }
@@ -919,7 +919,7 @@ __device__ __forceinline__ void walk_pair_step(Walk &a, Walk &b, const MatchShar
 // that make up much of source text)
 template <int K>
 __device__ __forceinline__ uint32_t walk_finish(const Walk &w, const MatchShared *s, const DeflateParams &P,
-                                                const uint32_t (&win)[9], uint32_t near, uint32_t lim4,
+                                                const uint32_t (&win)[9], uint32_t near, uint32_t lim4, uint32_t d4,
                                                 uint32_t &carry_len, uint32_t &carry_dist) {
   uint32_t best_len = w.best_len < w.cl ? w.cl : w.best_len, best_dist = w.best_dist;
   // a far 3-byte match (carried from the previous position) is dropped in
@@ -932,7 +932,6 @@ __device__ __forceinline__ uint32_t walk_finish(const Walk &w, const MatchShared
   // (positions from lim4 on have no 4-byte link: their keys would need bytes
   // past the segment's end)
   if (w.max_len >= 4 && short_ && w.p < lim4) {
-    const uint32_t d4 = s->link4[w.p & (DF_SUB - 1)];
     uint32_t qw[2];
     ld_run<2>(s, w.p - d4, qw);
     const uint32_t x0 = qw[0] ^ w.cur, x1 = qw[1] ^ w.cur2;
@@ -962,25 +961,32 @@ __device__ void search_quad(const MatchShared *s, const DeflateParams &P, uint32
   // are never used: near distances stay <= p)
   uint32_t w[9];
   ring_dwords<8>(s, ridx(pb - 16) >> 2, w);
+  // the four positions' 4-byte-table links (final: the super-step waited for
+  // them), read with the window so that walk_finish's lookups start from
+  // the candidate's bytes -- one LDS round trip each instead of two
+  const uint2 l4 = *reinterpret_cast<const uint2 *>(&s->link4[pb & (DF_SUB - 1)]);
+  // (and the four chain links the walks start from: positions 1 and 3 begin
+  // after 0 and 2 finish, their first link already in registers)
+  const uint2 l8 = *reinterpret_cast<const uint2 *>(&s->prev[ridx(pb)]);
   // positions 0 and 2 walk together, then 1 and 3 with the carry of 0 and 2
   uint32_t out[4];
   uint32_t c0l, c0d, c2l, c2d, cl, cd;
   const uint32_t nr0 = near_any<0, 1>(w, win32<16>(w), ~0u), nr1 = near_any<1, 1>(w, win32<17>(w), ~0u);
   const uint32_t nr2 = near_any<2, 1>(w, win32<18>(w), ~0u), nr3 = near_any<3, 1>(w, win32<19>(w), ~0u);
   Walk wa, wb;
-  walk_init(wa, s, P, pb, pml, win32<16>(w), win32<20>(w), win32<24>(w), win32<28>(w), 0, 0);
-  walk_init(wb, s, P, pb + 2, pml, win32<18>(w), win32<22>(w), win32<26>(w), win32<30>(w), 0, 0);
+  walk_init(wa, s, P, pb, pml, win32<16>(w), win32<20>(w), win32<24>(w), win32<28>(w), 0, 0, l8.x & 0xFFFFu);
+  walk_init(wb, s, P, pb + 2, pml, win32<18>(w), win32<22>(w), win32<26>(w), win32<30>(w), 0, 0, l8.y & 0xFFFFu);
   for (int step = 0; wa.active || wb.active; ++step) walk_pair_step(wa, wb, s, P, step);
-  out[0] = walk_finish<0>(wa, s, P, w, nr0, lim4, c0l, c0d);
-  out[2] = walk_finish<2>(wb, s, P, w, nr2, lim4, c2l, c2d);
+  out[0] = walk_finish<0>(wa, s, P, w, nr0, lim4, l4.x & 0xFFFFu, c0l, c0d);
+  out[2] = walk_finish<2>(wb, s, P, w, nr2, lim4, l4.y & 0xFFFFu, c2l, c2d);
 #ifdef ZT_DF_NOCARRY  // experiment: positions 1 and 3 start without the carried match
   c0l = c0d = c2l = c2d = 0;
 #endif
-  walk_init(wa, s, P, pb + 1, pml, win32<17>(w), win32<21>(w), win32<25>(w), win32<29>(w), c0l, c0d);
-  walk_init(wb, s, P, pb + 3, pml, win32<19>(w), win32<23>(w), win32<27>(w), win32<31>(w), c2l, c2d);
+  walk_init(wa, s, P, pb + 1, pml, win32<17>(w), win32<21>(w), win32<25>(w), win32<29>(w), c0l, c0d, l8.x >> 16);
+  walk_init(wb, s, P, pb + 3, pml, win32<19>(w), win32<23>(w), win32<27>(w), win32<31>(w), c2l, c2d, l8.y >> 16);
   for (int step = 0; wa.active || wb.active; ++step) walk_pair_step(wa, wb, s, P, step);
-  out[1] = walk_finish<1>(wa, s, P, w, nr1, lim4, cl, cd);
-  out[3] = walk_finish<3>(wb, s, P, w, nr3, lim4, cl, cd);
+  out[1] = walk_finish<1>(wa, s, P, w, nr1, lim4, l4.x >> 16, cl, cd);
+  out[3] = walk_finish<3>(wb, s, P, w, nr3, lim4, l4.y >> 16, cl, cd);
   // the positions' own bytes (res_pack)
   out[0] |= win32<16>(w) << 24;
   out[1] |= win32<17>(w) << 24;
