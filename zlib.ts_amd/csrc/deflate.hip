@@ -52,7 +52,8 @@ __device__ unsigned long long g_bk_time[8];  // debug: block_kernel phase cycles
 #define DF_T(v) (void)0
 #endif
 #ifdef ZT_DF_COUNT
-__device__ unsigned long long g_df_count[4];  // debug: pair steps (per wave), lane hops, extends (lanes), extends (waves)
+__device__ unsigned long long g_df_count[8];  // debug: pair steps (per wave), lane hops, extends (lanes), extends (waves),
+                                              // measured lanes that improve / measure < 8 bytes / do not improve
 #endif
 
 #ifndef ZT_DF_BLOCK
@@ -859,6 +860,10 @@ __device__ __forceinline__ void walk_extend(Walk &w, const MatchShared *s, const
   // pass runs with a few lanes of the wave, and every branch of the nest is
   // taken by one of them: match 21.0 -> 20.3 ms per GiB, streams identical)
   const bool upd = len >= 3 && len > w.best_len;
+#ifdef ZT_DF_COUNT
+  atomicAdd(&g_df_count[upd ? 4 : 6], 1ull);
+  if (len < 8) atomicAdd(&g_df_count[5], 1ull);
+#endif
   const bool stop = upd && ((int)len >= P.nice_len || len >= w.max_len);
   const bool newo = upd && !stop && len >= 4;
   w.best_len = upd ? len : w.best_len;
@@ -2939,8 +2944,8 @@ extern "C" int zt_debug_bk_time(unsigned long long *out) {
 
 #ifdef ZT_DF_COUNT
 extern "C" int zt_debug_df_count(unsigned long long *out) {
-  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_df_count), sizeof(unsigned long long) * 4);
-  unsigned long long z[4] = {};
+  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_df_count), sizeof(unsigned long long) * 8);
+  unsigned long long z[8] = {};
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_df_count), z, sizeof z);
   return 0;
 }
