@@ -146,6 +146,9 @@ struct LaneBits {
   const uint32_t *stage;
   uint32_t qbase;
   uint32_t q;      // next dword to shift in
+  uint32_t nw;     // that dword, read ahead: a refill is register work, off the
+                   // token chain's LDS round trips (the read for the next one
+                   // is issued before the token's table read)
   uint64_t bb;
   uint32_t bc;
   uint32_t rel;    // bit position of bb bit 0, relative to the body start
@@ -157,17 +160,20 @@ struct LaneBits {
   __device__ __forceinline__ void init(uint64_t abs_bit, uint32_t rel0) {
     q = (uint32_t)(abs_bit >> 5);
     const uint32_t sh = (uint32_t)abs_bit & 31;
-    bb = word(q) >> sh;
-    bc = 32 - sh;
-    ++q;
+    const uint32_t w0 = word(q), w1 = word(q + 1);
+    nw = word(q + 2);
+    bb = ((((uint64_t)w1) << 32) | w0) >> sh;
+    bc = 64 - sh;
+    q += 2;
     rel = rel0;
   }
   // afterwards at least 32 valid bits
   __device__ __forceinline__ void refill() {
     if (bc <= 32) {
-      bb |= (uint64_t)word(q) << bc;
+      bb |= (uint64_t)nw << bc;
       bc += 32;
       ++q;
+      nw = word(q);
     }
   }
   __device__ __forceinline__ void consume(uint32_t n) {
@@ -242,6 +248,46 @@ __device__ __forceinline__ int lane_token(LaneBits &lb, const HuffTab *lt, const
   lb.consume(dcl + dex);
   tok = (length << 16) | dist;
   nbytes = length;
+  return 0;
+}
+
+// lane_token for the first pass and the repairs: the token's bits consumed,
+// its value not formed (same outcomes and bit positions)
+__device__ __forceinline__ int lane_skip(LaneBits &lb, const HuffTab *lt, const HuffTab *dt) {
+  constexpr uint32_t M = (1u << PRI) - 1;
+  lb.refill();
+  const uint32_t e = lt->pri[(uint32_t)lb.bb & M];
+  uint32_t cl, sym, ex;
+  if (e & 15) {
+    cl = e & 15;
+    sym = (e >> 8) & 511;
+    ex = (e >> 4) & 15;
+  } else {
+    const int s = long_code_lane(lt, (uint32_t)lb.bb, cl);
+    if (s < 0) return -1;
+    sym = (uint32_t)s;
+    ex = sym > 256 ? len_extra(sym - 257) : 0;
+  }
+  if (sym <= 256) {
+    lb.consume(cl);
+    return sym == 256 ? 1 : 0;
+  }
+  lb.consume(cl + ex);
+  lb.refill();
+  const uint32_t d = dt->pri[(uint32_t)lb.bb & M];
+  uint32_t dcl, dsym, dex;
+  if (d & 15) {
+    dcl = d & 15;
+    dsym = (d >> 8) & 511;
+    dex = (d >> 4) & 15;
+  } else {
+    const int s = long_code_lane(dt, (uint32_t)lb.bb, dcl);
+    if (s < 0) return -1;
+    dsym = (uint32_t)s;
+    dex = dsym < 30 ? dist_extra(dsym) : 0;
+  }
+  if (dsym >= 30) return -1;
+  lb.consume(dcl + dex);
   return 0;
 }
 
@@ -363,11 +409,11 @@ __device__ uint64_t lane_phase_map(const LaneBits &lb, uint64_t b0, uint32_t s_l
       d[k].ph = 15;
       d[k].act = in_range && x0 + k < xmax;
     }
-    for (;;) {
+    for (;;) {  // (per lane: a lane whose phases are all mapped leaves exec; C2 tokenize 5.15 -> 5.03 ms, r05ak)
       bool any = false;
 #pragma unroll
       for (int k = 0; k < PM_N; ++k) any = any || d[k].act;
-      if (!__ballot(any)) break;
+      if (!any) break;
       uint32_t w[PM_N], e[PM_N];
 #pragma unroll
       for (int k = 0; k < PM_N; ++k) {
@@ -391,6 +437,7 @@ __device__ uint64_t lane_phase_map(const LaneBits &lb, uint64_t b0, uint32_t s_l
         } else {
           LaneBits t = lb;
           t.q = r.q;
+          t.nw = w[k];  // = word(r.q)
           t.bb = r.bb;
           t.bc = r.bc;
           t.rel = r.rel;
@@ -554,7 +601,6 @@ __device__ int tok_huffman_simt(Reader &rd, uint64_t b0, const HuffTab *lt, cons
       if (iter > 66) return ZT_E_INPUT_BROKEN;
       bool active = todo;
       uint32_t cw = 0, cwi = 0;  // bitmap word being assembled, its index
-      uint32_t merge = 0xFFFFFFFFu;
       if (active) {
         lb.init(b0 + from, from);
         cwi = (from - s_l) >> 5;
@@ -563,37 +609,36 @@ __device__ int tok_huffman_simt(Reader &rd, uint64_t b0, const HuffTab *lt, cons
         // marks below a repair's start are off every path it can merge with
         for (uint32_t x = 0; x < cwi; ++x) sp->bm[x][lane] = 0;
       }
-      while (__ballot(active)) {
-        if (active) {
-          const uint32_t p = lb.rel - s_l;  // < SP_LANE_BITS while decoding this lane's range
-          const uint32_t wi = p >> 5;
-          if (wi != cwi) {
-            // leave word cwi: new marks below, on a repair old marks are stale
-            sp->bm[cwi][lane] = cw;
-            for (uint32_t x = cwi + 1; x < wi; ++x) sp->bm[x][lane] = 0;
-            cwi = wi;
-            cw = 0;
-          }
-          if (repair && ((sp->bm[wi][lane] >> (p & 31)) & 1)) {
-            // merged with the old path: the old marks from p on are right
-            merge = p;
-            const uint32_t below = (p & 31) ? (0xFFFFFFFFu >> (32 - (p & 31))) : 0u;
-            sp->bm[wi][lane] = (cw & below) | (sp->bm[wi][lane] & ~below);
+      // (a per-lane loop: finished lanes leave exec with their registers
+      // untouched, where a wave loop around `if (active)` copied the carried
+      // state every iteration -- tokenize 3.86 -> 3.60 ms per GiB, r05ai)
+      while (active) {
+        const uint32_t p = lb.rel - s_l;  // < SP_LANE_BITS while decoding this lane's range
+        const uint32_t wi = p >> 5;
+        if (wi != cwi) {
+          // leave word cwi: new marks below, on a repair old marks are stale
+          sp->bm[cwi][lane] = cw;
+          for (uint32_t x = cwi + 1; x < wi; ++x) sp->bm[x][lane] = 0;
+          cwi = wi;
+          cw = 0;
+        }
+        if (repair && ((sp->bm[wi][lane] >> (p & 31)) & 1)) {
+          // merged with the old path: the old marks from p on are right
+          const uint32_t below = (p & 31) ? (0xFFFFFFFFu >> (32 - (p & 31))) : 0u;
+          sp->bm[wi][lane] = (cw & below) | (sp->bm[wi][lane] & ~below);
+          active = false;
+        } else {
+          cw |= 1u << (p & 31);
+          if (lb.rel >= stop_rel) {
+            // a token starts at or after the stop: the unit ends here
+            flags = 3;
+            ev_pos = s_l + p;
+            end = ev_pos;
             active = false;
           } else {
-            cw |= 1u << (p & 31);
-            uint32_t tk, nb;
-            if (lb.rel >= stop_rel) {
-              // a token starts at or after the stop: the unit ends here
-              flags = 3;
-              ev_pos = s_l + p;
-              end = ev_pos;
-              active = false;
-            } else {
-            const int r = lane_token(lb, lt, dt, tk, nb);
+            const int r = lane_skip(lb, lt, dt);
             if (r != 0 || lb.rel > limit) {
               flags = r > 0 ? 1 : 2;
-              ev_pos = lb.rel - 0;  // provisional; fixed below
               ev_pos = s_l + p;
               end = lb.rel;
               active = false;
@@ -602,11 +647,10 @@ __device__ int tok_huffman_simt(Reader &rd, uint64_t b0, const HuffTab *lt, cons
               flags = 0;
               active = false;
             }
-            }
-            if (!active) {
-              sp->bm[cwi][lane] = cw;
-              for (uint32_t x = cwi + 1; x < SP_WORDS; ++x) sp->bm[x][lane] = 0;
-            }
+          }
+          if (!active) {
+            sp->bm[cwi][lane] = cw;
+            for (uint32_t x = cwi + 1; x < SP_WORDS; ++x) sp->bm[x][lane] = 0;
           }
         }
       }
@@ -673,7 +717,6 @@ __device__ int tok_huffman_simt(Reader &rd, uint64_t b0, const HuffTab *lt, cons
       todo = in_range && !synced && t >= s_l && tp < SP_LANE_BITS;
       if (todo) from = t;
       repair = true;
-      (void)merge;
     }
     TK_T(tt3);
     // final per-lane state: true start t, tokens = marks in [t, ev or end)
@@ -870,12 +913,14 @@ constexpr int cp_vmcnt(uint32_t v) { return (int)(0x0F70u | (v & 15u) | ((v >> 4
 // CP_STEP) reads are in flight (one 1 KiB LDS-DMA each, dsrc 1 KiB aligned,
 // its buffer padded by a chunk), and the step's own have landed
 typedef unsigned int cp_u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void cp_desc_fetch(const uint16_t *dsrc, uint16_t *ring, uint64_t op, uint64_t n,
-                                              uint64_t &issued, int lane) {
-  const uint64_t nchunks = (n + CP_CHUNK - 1) / CP_CHUNK;
-  const uint64_t need0 = (op + CP_STEP + CP_CHUNK - 1) / CP_CHUNK;
-  const uint64_t need = need0 < nchunks ? need0 : nchunks;
-  const uint64_t want = need + CP_AHEAD < nchunks ? need + CP_AHEAD : nchunks;
+// (U: the offset type -- uint32_t for segments below 2^31 bytes, where every
+// index here stays below 2^32 and the bookkeeping is 32-bit scalar work)
+template <typename U = uint64_t>
+__device__ __forceinline__ void cp_desc_fetch(const uint16_t *dsrc, uint16_t *ring, U op, U n, U &issued, int lane) {
+  const U nchunks = (n + CP_CHUNK - 1) / CP_CHUNK;
+  const U need0 = (op + CP_STEP + CP_CHUNK - 1) / CP_CHUNK;
+  const U need = need0 < nchunks ? need0 : nchunks;
+  const U want = need + CP_AHEAD < nchunks ? need + CP_AHEAD : nchunks;
   while (issued < want) {
     __builtin_amdgcn_global_load_lds(reinterpret_cast<const cp_u32x4 *>(dsrc + issued * CP_CHUNK) + lane,
                                      ring + ((issued * CP_CHUNK) & (CP_DESC_RING - 1)), 16, 0, 0);

@@ -485,22 +485,24 @@ struct CopyShared {
 };
 
 // ring bytes [lo, hi) (segment positions) to out + lo
-__device__ __forceinline__ void cp_flush(const CopyShared *sh, uint8_t *out, uint64_t lo, uint64_t hi, int lane) {
+template <typename U>
+__device__ __forceinline__ void cp_flush(const CopyShared *sh, uint8_t *out, U lo, U hi, int lane) {
   if (lo >= hi) return;
   if (hi - lo == RS_FLUSH && (((uintptr_t)out + lo) & 15) == 0) {
     // a whole granule: every ring read in flight before the stores
     constexpr int K = RS_FLUSH / 1024;
     u32x4r v[K];
+    uint8_t *o = out + lo;
 #pragma unroll
     for (int k = 0; k < K; ++k)
-      v[k] = *reinterpret_cast<const u32x4r *>(&sh->ring[(lo + (uint64_t)lane * 16 + 1024 * k) & RING_MASK]);
+      v[k] = *reinterpret_cast<const u32x4r *>(&sh->ring[((uint32_t)lo + (uint32_t)lane * 16 + 1024 * k) & RING_MASK]);
 #pragma unroll
-    for (int k = 0; k < K; ++k) *reinterpret_cast<u32x4r *>(out + lo + (uint64_t)lane * 16 + 1024 * k) = v[k];
+    for (int k = 0; k < K; ++k) *reinterpret_cast<u32x4r *>(o + (uint32_t)lane * 16 + 1024 * k) = v[k];
   } else if ((((uintptr_t)out + lo) & 15) == 0 && ((hi - lo) & 15) == 0) {
-    for (uint64_t p = lo + (uint64_t)lane * 16; p < hi; p += 1024)
+    for (U p = lo + (U)lane * 16; p < hi; p += 1024)
       *reinterpret_cast<u32x4r *>(out + p) = *reinterpret_cast<const u32x4r *>(&sh->ring[p & RING_MASK]);
   } else {
-    for (uint64_t p = lo + lane; p < hi; p += 64) out[p] = sh->ring[p & RING_MASK];
+    for (U p = lo + lane; p < hi; p += 64) out[p] = sh->ring[p & RING_MASK];
   }
 }
 
@@ -536,31 +538,19 @@ __device__ unsigned long long g_cp_time[8];  // debug: copy_kernel cycles per ph
 #else
 #define CP_T(v) (void)0
 #endif
-__global__ __launch_bounds__(64) void copy_kernel(ResolveParams P) {
-  __shared__ CopyShared sh;
+// one segment's bytes [0, n) from its descriptors; U is the offset type
+// (uint32_t below 2^31 bytes: the per-step bookkeeping is 32-bit)
+template <typename U>
+__device__ __forceinline__ void copy_run(CopyShared &sh, uint8_t *out, const uint16_t *dsrc, const U n, const int lane) {
 #ifdef ZT_CP_TIME
   unsigned long long cp_acc[4] = {0, 0, 0, 0}, ct0 = 0, ct1 = 0, ct2 = 0, ct3 = 0, ct4 = 0, nsteps = 0;
 #endif
-  const uint32_t sg = blockIdx.x;
-  const int lane = threadIdx.x & 63;
-  // device-built chain: launched for the bound on its segments
-  if (P.info && (!P.info->ok || sg >= P.info->nseg)) return;
-  SegJob sj = P.segs[sg];
-  if (sj.count >> 31) {  // stored runs only: expand_kernel wrote the bytes
-    if (lane == 0) P.seg_status[sg] = ZT_OK;
-    return;
-  }
-  const uint64_t seg_out = P.units[sj.first].out_off;
-  const ChainUnit lastu = P.units[sj.first + sj.count - 1];
-  const uint64_t n = lastu.out_off + lastu.out_len - seg_out;  // segment bytes
-  uint8_t *out = P.out + seg_out;
-  const uint16_t *dsrc = P.desc + P.units[sj.first].desc_off;  // 512-aligned (cp_desc_fetch's chunks)
-  uint64_t issued = 0, flushed = 0;
+  U issued = 0, flushed = 0;
   // lane j: bytes op + 256 g + 4 j .. + 3 for each group g (bytes past n are
   // never flushed).  The next step's descriptors are fetched and read right
   // after this step's ring writes, so a step starts with its ring reads.
   uint64_t dd[CP_G];
-  auto read_desc = [&](uint64_t o) {
+  auto read_desc = [&](U o) {
 #pragma unroll
     for (int g = 0; g < CP_G; ++g) {
       const uint32_t x = (uint32_t)o + 256u * g + 4 * (uint32_t)lane;  // ring / descriptor index (masked)
@@ -568,10 +558,10 @@ __global__ __launch_bounds__(64) void copy_kernel(ResolveParams P) {
     }
   };
   if (n) {
-    cp_desc_fetch(dsrc, sh.desc, 0, n, issued, lane);
+    cp_desc_fetch<U>(dsrc, sh.desc, 0, n, issued, lane);
     read_desc(0);
   }
-  for (uint64_t op = 0; op < n; op += CP_STEP) {
+  for (U op = 0; op < n; op += CP_STEP) {
     CP_T(ct0);
     // every byte of a step is a literal or a ring byte before the step, so
     // all ring reads are issued before any write
@@ -600,7 +590,7 @@ __global__ __launch_bounds__(64) void copy_kernel(ResolveParams P) {
       // a unit boundary inside this step left references into it: resolve
       // them byte by byte (64-byte sub-steps, pointer jumping)
       for (uint32_t sub = 0; sub < CP_STEP; sub += 64) {
-        const uint64_t y = op + sub + (uint64_t)lane;
+        const U y = op + sub + (U)lane;
         const uint32_t d = y < n ? sh.desc[y & (CP_DESC_RING - 1)] : 0x8000u;  // (past n: stale)
         int32_t off;
         uint32_t val = cp_byte(&sh, op, d, off);
@@ -632,13 +622,13 @@ __global__ __launch_bounds__(64) void copy_kernel(ResolveParams P) {
     wave_sync();
     CP_T(ct3);
     if (op + CP_STEP < n) {
-      cp_desc_fetch(dsrc, sh.desc, op + CP_STEP, n, issued, lane);
+      cp_desc_fetch<U>(dsrc, sh.desc, op + CP_STEP, n, issued, lane);
       read_desc(op + CP_STEP);
     }
     CP_T(ct1);
-    const uint64_t end = op + CP_STEP < n ? op + CP_STEP : n;
+    const U end = op + CP_STEP < n ? op + CP_STEP : n;
     if (end - flushed >= RS_FLUSH) {
-      const uint64_t upto = flushed + RS_FLUSH;
+      const U upto = flushed + RS_FLUSH;
       cp_flush(&sh, out, flushed, upto, lane);
       flushed = upto;
 #ifdef ZT_CP_FLUSH_WAIT
@@ -666,6 +656,28 @@ __global__ __launch_bounds__(64) void copy_kernel(ResolveParams P) {
 #endif
   wave_sync();
   cp_flush(&sh, out, flushed, n, lane);
+}
+
+__global__ __launch_bounds__(64) void copy_kernel(ResolveParams P) {
+  __shared__ CopyShared sh;
+  const uint32_t sg = blockIdx.x;
+  const int lane = threadIdx.x & 63;
+  // device-built chain: launched for the bound on its segments
+  if (P.info && (!P.info->ok || sg >= P.info->nseg)) return;
+  SegJob sj = P.segs[sg];
+  if (sj.count >> 31) {  // stored runs only: expand_kernel wrote the bytes
+    if (lane == 0) P.seg_status[sg] = ZT_OK;
+    return;
+  }
+  const uint64_t seg_out = P.units[sj.first].out_off;
+  const ChainUnit lastu = P.units[sj.first + sj.count - 1];
+  const uint64_t n = lastu.out_off + lastu.out_len - seg_out;  // segment bytes
+  uint8_t *out = P.out + seg_out;
+  const uint16_t *dsrc = P.desc + P.units[sj.first].desc_off;  // 512-aligned (cp_desc_fetch's chunks)
+  if (n < (1ull << 31))
+    copy_run<uint32_t>(sh, out, dsrc, (uint32_t)n, lane);
+  else
+    copy_run<uint64_t>(sh, out, dsrc, n, lane);
   if (lane == 0) P.seg_status[sg] = ZT_OK;
 }
 
