@@ -36,6 +36,9 @@ struct TokShared {
   HuffTab lit;
   HuffTab dist;
   uint8_t lens[320];
+#ifdef ZT_TOK_LDS_PAD
+  uint8_t pad[ZT_TOK_LDS_PAD];  // (measurement: occupancy held to a larger table's)
+#endif
 };
 
 
