@@ -1831,14 +1831,21 @@ __global__ __launch_bounds__(64, ZT_OP_MINW) void optparse_kernel(DeflateParams 
               // one add3 of pre-shifted terms (exact modulo 2^32: the
               // unshifted value is below 2^23)
               const uint32_t base9 = (uint32_t)(dc + 0x8000 - (int)C1) << 9;
+              // a pair of cut lengths enters when both are valid (one compare
+              // and one select per pair: optparse 2.63 -> 2.41 ms per GiB with
+              // two selects under one compare, r05au); the odd length L
+              // itself, whose pair does not, is the full-length candidate
+              // below, taken for every match (the same key: C[i + L] from the
+              // ring)
 #pragma unroll
               for (uint32_t l = 3; l < OP_SHORT; l += 2) {
                 const uint32_t ka = base9 + cr9[l] + lk[l], kb = base9 + cr9[l + 1] + lk[l + 1];
-                key = op_min3(key, l <= L ? ka : 0xFFFFFFFFu, l + 1 <= L ? kb : 0xFFFFFFFFu);
+                const uint32_t m = op_min3(key, ka, kb);
+                key = l + 1 <= L ? m : key;
               }
               {
                 const uint32_t kl = ((uint32_t)(dc + 0x8000 + c_far) << 9) | (Lc & 511);
-                key = (L > OP_SHORT && kl < key) ? kl : key;
+                key = (L >= 3 && kl < key) ? kl : key;
               }
               const uint32_t choice = key & 511;
               const int best = (int)(key >> 9) - 0x8000;
