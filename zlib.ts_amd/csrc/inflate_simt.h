@@ -127,9 +127,9 @@ __device__ __forceinline__ int tok_huffman(Reader &rd, const HuffTab *lt, const 
 // and the marks are corrected on the way.  A second pass decodes every lane's
 // exact range and writes its tokens at their final index.
 #ifndef ZT_SP_LANE_BITS
-#define ZT_SP_LANE_BITS 480
+#define ZT_SP_LANE_BITS 448  // 416 / 448 / 480: tokenize 3.78 / 3.41 / 3.48 ms per GiB with the per-lane first pass (gpurun_out/r05bb)
 #endif
-constexpr uint32_t SP_LANE_BITS = ZT_SP_LANE_BITS;        // 60 bytes per lane: 18.5 KiB of LDS, 8 units per CU
+constexpr uint32_t SP_LANE_BITS = ZT_SP_LANE_BITS;        // 56 bytes per lane
 constexpr uint32_t SP_WORDS = SP_LANE_BITS / 32;          // bitmap words per lane
 constexpr uint32_t SP_STAGE_BYTES = IN_RING;              // staged input per round
 static_assert(64 * SP_LANE_BITS / 8 + 16 + 64 <= SP_STAGE_BYTES, "round must fit the stage");
