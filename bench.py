@@ -39,9 +39,13 @@ the LZ77 match finder; algorithmic bytes = N input bytes per launch, SURVEY.md
 -- the C restatement of the reference's RawDeflate + RawInflate -- on a
 bounded sample on 16 threads, one-core figure beside it, rank 0, N = 1
 only), the per-generator compression ratio of
-this build against the reference on that sample, and `api` -- the same round
+this build against the reference on that sample, `api` -- the same round
 trip through the host-buffer entry points (zt_deflate_raw / zt_inflate_raw),
-PCIe transfers included (rank 0, N = 1, weak mode only).
+PCIe transfers included -- `api_node` -- that round trip from Node through
+the JS facade and the N-API addon, the boundary north_star names -- and
+`per_generator` -- deflate / inflate rates of each generator alone, the
+source-text sample included (all rank 0, N = 1, weak mode only; none of
+them inside the timed region).
 """
 import argparse
 import hashlib
@@ -71,6 +75,8 @@ def parse_args(argv=None):
     ap.add_argument("--mode", choices=["weak", "c3"], default="weak")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-api", action="store_true", help="skip the host-buffer (PCIe-inclusive) round trip")
+    ap.add_argument("--no-node", action="store_true", help="skip the Node (N-API facade) round trip")
+    ap.add_argument("--no-per-generator", action="store_true", help="skip the per-generator rates")
     a = ap.parse_args(argv)
     if a.size is None:
         a.size = (8 << 30) if a.mode == "c3" else (1 << 30)
@@ -273,6 +279,100 @@ def api_roundtrip(d_in, n, level, zt):
                     "outputs registered them, ZT_HOST_POOL_MB)"}
 
 
+def api_node(d_in, api):
+    """The same round trip from Node through the drop-in boundary north_star
+    names (the zlib.ts_amd facade over the N-API addon zt.node):
+    new RawDeflate(u8).compress() and new RawInflate(s).decompress() on a
+    host copy of the corpus (tools/node_bench.mjs: median of 3 calls after a
+    warm-up, each after the previous results were collected), plus the
+    C0-shaped 64 KiB per-call latency; `vs_api` = the Node rate / the C-ABI
+    rate of `api` (1.0 = no boundary overhead)."""
+    import shutil
+    import tempfile
+
+    node = shutil.which("node")
+    addon = os.path.join(HERE, "zlib.ts_amd", "zt.node")
+    if not node or not os.path.exists(addon):
+        return {"skipped": "node or zlib.ts_amd/zt.node missing"}
+    tmpdir = "/dev/shm" if os.path.isdir("/dev/shm") else None
+    with tempfile.NamedTemporaryFile(dir=tmpdir, suffix=".bin", delete=False) as f:
+        path = f.name
+        d_in.cpu().numpy().tofile(f)
+    try:
+        p = subprocess.run([node, "--expose-gc", os.path.join(HERE, "tools", "node_bench.mjs"), path, "3"],
+                           capture_output=True, text=True, timeout=600)
+    finally:
+        os.unlink(path)
+    if p.returncode != 0:
+        raise SystemExit("bench: node bench failed: " + p.stderr[-2000:])
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    if api:
+        r["vs_api"] = {k: round(r[k] / api[k], 3) for k in ("deflate_GiBps", "inflate_GiBps", "roundtrip_GiBps")
+                       if api.get(k)}
+    r["note"] = ("Node " + r.get("node", "") + ": zlib.ts_amd/lib RawDeflate / RawInflate over zt.node (results are "
+                 "external ArrayBuffers over libzt's host output pool, no copy), 1 GiB corpus read from a file; "
+                 "median of 3 timed calls after one warm-up")
+    return r
+
+
+def source_text(limit=4 << 20):
+    """SURVEY 8(d)'s realistic generator: the image's /usr/lib/python3.10/*.py
+    concatenated in name order, first `limit` bytes (None if absent)."""
+    d = "/usr/lib/python3.10"
+    if not os.path.isdir(d):
+        return None
+    out = bytearray()
+    for name in sorted(os.listdir(d)):
+        if name.endswith(".py"):
+            with open(os.path.join(d, name), "rb") as f:
+                out += f.read()
+            if len(out) >= limit:
+                break
+    return bytes(out[:limit]) if len(out) >= limit else None
+
+
+def per_generator(d_in, n, level, dplan, iplan, d_c, d_out, zt):
+    """Untimed by the headline: deflate and inflate of `n` bytes of ONE
+    generator each (wordsalad, structured int32 deltas, xorshift32 -- device
+    synthetic -- and the source-text sample tiled to n bytes), the mean of 3
+    calls after a warm-up through the same device plans as the timed step;
+    per kind the ratio, the deflate pipeline and match kernel times and the
+    inflate time (HIP events).  Overwrites d_in."""
+    import torch
+
+    out = {}
+    src = source_text()
+    kinds = ["wordsalad", "structured", "xorshift32"] + (["source_text"] if src else [])
+    for kind in kinds:
+        if kind == "source_text":
+            tile = torch.frombuffer(bytearray(src), dtype=torch.uint8).cuda()
+            reps = (n + len(src) - 1) // len(src)
+            d_in[:n] = tile.repeat(reps)[:n]
+        else:
+            zt.synth_dev(kind, 11, d_in.data_ptr(), n)
+        clen = dplan.run(d_in.data_ptr(), n, d_c.data_ptr())
+        olen, _ = iplan.run(d_c.data_ptr(), clen, d_out.data_ptr(), d_out.numel())
+        torch.cuda.synchronize()
+        if olen != n or not torch.equal(d_out[:n], d_in[:n]):
+            raise SystemExit(f"bench: per-generator round trip mismatch ({kind})")
+        zt.timing_enable(True)
+        for _ in range(3):
+            clen = dplan.run(d_in.data_ptr(), n, d_c.data_ptr())
+            iplan.run(d_c.data_ptr(), clen, d_out.data_ptr(), d_out.numel())
+        torch.cuda.synchronize()
+        t = zt.timing_read()
+        zt.timing_enable(False)
+        k = lambda a, b: t[a] / max(1, t[b])
+        pipe, match, inf = k("deflate_pipeline_ms", "deflate_pipelines"), k("deflate_ms", "deflate_launches"), \
+            k("inflate_ms", "inflate_launches")
+        out[kind] = {"ratio": round(clen / n, 5), "deflate_GiBps": round(n / 2**30 / (pipe * 1e-3), 2),
+                     "inflate_GiBps": round(n / 2**30 / (inf * 1e-3), 2), "deflate_pipeline_ms": round(pipe, 3),
+                     "match_kernel_ms": round(match, 3), "inflate_ms": round(inf, 3)}
+    out["note"] = (f"{n / 2**30:g} GiB of one generator each, level {level}, device-resident, mean of 3 after a "
+                   "warm-up (HIP events); source_text = /usr/lib/python3.10/*.py, first 4 MiB, tiled")
+    return out
+
+
 # ---------------------------------------------------------------- ranks
 def run_rank(args):
     import torch
@@ -414,6 +514,10 @@ def run_rank(args):
             line["ratio_vs_ref"] = ratios
         if not args.no_api:
             line["api"] = api_roundtrip(d_in[:n], n, args.level, zt)
+            if not args.no_node:
+                line["api_node"] = api_node(d_in[:n], line["api"])
+        if not args.no_per_generator:
+            line["per_generator"] = per_generator(d_in, n, args.level, dplan, iplan, d_c, d_out, zt)
     if rank == 0:
         print(json.dumps(line), flush=True)
     dplan.close()

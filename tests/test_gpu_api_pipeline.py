@@ -172,3 +172,97 @@ def test_host_output_pool_round_trips(zt):
             zt.lib.zt_free(back)
     assert np.array_equal(np.ctypeslib.as_array(held[0], shape=(n,)), host)
     zt.lib.zt_free(held[0])
+
+
+# ---- round 6: the pipelined inflate at any output ratio, and its error paths
+# (the output was sized 4x the input and a piece past it sent the
+# whole stream to the one-call decode; a failing pipeline returned its output
+# buffer while copies into it could still be running)
+
+def _pieces_decoded(zt, fn):
+    """Run fn() and return how many decodes the segment path made (the
+    pipelined call makes one per piece; the one-call decode makes one)."""
+    zt.timing_enable(True)
+    r = fn()
+    paths = zt.timing_read()["inflate_paths"]
+    zt.timing_enable(False)
+    return r, paths[0]
+
+
+def test_pipelined_inflate_high_ratio_stays_pipelined(zt):
+    """wordsalad at level 6 compresses ~6.5:1: every piece stays in the
+    pipeline (no second decode of the whole stream), output exact."""
+    import numpy as np
+    import torch
+
+    n = 256 << 20
+    d_in = torch.empty(n, dtype=torch.uint8, device="cuda")
+    zt.synth_dev("wordsalad", 12, d_in.data_ptr(), n)
+    host = d_in.cpu().numpy()
+    s = _device_stream(zt, torch, d_in, n, 6)
+    assert len(s) >= 32 << 20 and n > 4 * len(s)
+    (back, ip), decodes = _pieces_decoded(zt, lambda: zt.inflate_raw(s))
+    assert ip == len(s) and len(back) == n
+    assert np.array_equal(np.frombuffer(back, dtype=np.uint8), host)
+    assert decodes >= 2, "the stream left the pipeline"
+
+
+def test_pipelined_inflate_ratio_jump_grows_outputs(zt):
+    """Piece 0 is incompressible (ratio 1) and the last piece holds 192 MiB
+    of one repeated byte: its device slot and the host output both grow
+    (one more decode of that piece, one move of the bytes so far) and the
+    result equals the data."""
+    import numpy as np
+    import torch
+
+    a, z = 40 << 20, 192 << 20
+    d_in = torch.empty(a + z, dtype=torch.uint8, device="cuda")
+    zt.synth_dev("xorshift32", 5, d_in.data_ptr(), a)
+    d_in[a:] = 0x61
+    host = d_in.cpu().numpy()
+    s = _device_stream(zt, torch, d_in, a + z, 6)
+    assert len(s) >= 32 << 20
+    (back, ip), decodes = _pieces_decoded(zt, lambda: zt.inflate_raw(s))
+    assert ip == len(s) and len(back) == a + z
+    assert np.array_equal(np.frombuffer(back, dtype=np.uint8), host)
+    assert decodes >= 2, "the stream left the pipeline"
+
+
+def test_pipelined_inflate_failure_on_registered_output(zt):
+    """A pipelined inflate that fails in its last piece after earlier pieces
+    were copied straight into a registered pool buffer: the call returns the
+    stream's error (or its one-call result) only after every copy finished,
+    and the pool stays usable -- the good stream decodes exactly afterwards."""
+    import ctypes
+
+    import numpy as np
+    import torch
+
+    n = 192 << 20
+    d_in = torch.empty(n, dtype=torch.uint8, device="cuda")
+    zt.synth_dev("mixed", 31, d_in.data_ptr(), n)
+    host = d_in.cpu().numpy()
+    s = _device_stream(zt, torch, d_in, n, 6)
+    iopts = zt.InflateOpts(1, 0x8000, 0)
+
+    def inflate(buf):
+        arr = np.frombuffer(buf, dtype=np.uint8)
+        back = ctypes.POINTER(ctypes.c_uint8)()
+        blen, ip = ctypes.c_size_t(), ctypes.c_size_t()
+        rc = zt.lib.zt_inflate_raw(arr.ctypes.data_as(ctypes.c_void_p), len(buf), 0, ctypes.byref(iopts),
+                                   ctypes.byref(back), ctypes.byref(blen), ctypes.byref(ip))
+        out = np.ctypeslib.as_array(back, shape=(blen.value,)).copy() if rc == 0 else None
+        if rc == 0:
+            zt.lib.zt_free(back)
+        return rc, out
+
+    for _ in range(2):  # the second output comes from the (now registered) pool
+        rc, out = inflate(s)
+        assert rc == 0 and np.array_equal(out, host)
+    bad = bytearray(s)
+    bad[-(256 << 10):-64] = b"\xff" * ((256 << 10) - 64)  # the last piece's blocks: broken
+    for _ in range(3):
+        rc, out = inflate(bytes(bad))
+        assert rc != 0 or len(out) != n or not np.array_equal(out, host)
+    rc, out = inflate(s)
+    assert rc == 0 and np.array_equal(out, host)

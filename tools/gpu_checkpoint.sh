@@ -17,7 +17,7 @@ tail -1 gpurun_out/${TAG}_bench.log
 # the 16-window ratio gate of this build (one gate log per checkpoint)
 timeout -k 10 300 python3 tools/ratio_gate.py > gpurun_out/${TAG}_gate.log 2>&1
 tail -1 gpurun_out/${TAG}_gate.log
-cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d $R/gpurun_out/${TAG}_prof -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-api > $R/gpurun_out/${TAG}_prof.log 2>&1
+cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d $R/gpurun_out/${TAG}_prof -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-api --no-per-generator > $R/gpurun_out/${TAG}_prof.log 2>&1
 cd $R
 cp gpurun_out/${TAG}_prof/run_kernel_stats.csv gpurun_out/${TAG}_kernel_stats.csv
 cut -d, -f1-4 gpurun_out/${TAG}_kernel_stats.csv | head -14

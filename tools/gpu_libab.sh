@@ -18,6 +18,6 @@ for L in "$@"; do
   if [ -z "$NOGATE" ]; then
     timeout -k 10 300 python tools/ratio_gate.py "${PARAMS:-}" > $O/gate_$n.log 2>&1
   fi
-  timeout -k 10 300 python bench.py --steps ${STEPS:-5} --warmup 2 --no-cpu-baseline --no-api > $O/bench_$n.log 2>&1
+  timeout -k 10 300 python bench.py --steps ${STEPS:-5} --warmup 2 --no-cpu-baseline --no-api --no-per-generator > $O/bench_$n.log 2>&1
   echo "$L | $(grep -o 'worst.*' $O/gate_$n.log 2>/dev/null) | $(tail -1 $O/bench_$n.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print("bench", d["value"], "ratio", d["ratio"], "deflate", d["deflate_pipeline_ms"], "match", d["match_kernel_ms"], "inflate", d["inflate_kernel_ms"])')"
 done

@@ -7,8 +7,8 @@ set -e
 TAG=${1:-r04sq}
 R=$GRAFT_REPO_ROOT; mkdir -p gpurun_out/$TAG; export TMPDIR=/tmp
 cd /tmp
-timeout -s KILL 150 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS -f csv -d $R/gpurun_out/$TAG/sq1 -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-api > $R/gpurun_out/$TAG/sq1.log 2>&1
-timeout -s KILL 150 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_ADDR_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_SCA -f csv -d $R/gpurun_out/$TAG/sq2 -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-api > $R/gpurun_out/$TAG/sq2.log 2>&1
+timeout -s KILL 150 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS -f csv -d $R/gpurun_out/$TAG/sq1 -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-api --no-per-generator > $R/gpurun_out/$TAG/sq1.log 2>&1
+timeout -s KILL 150 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_ADDR_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_SCA -f csv -d $R/gpurun_out/$TAG/sq2 -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-api --no-per-generator > $R/gpurun_out/$TAG/sq2.log 2>&1
 cd $R
 python3 tools/sq_summ.py gpurun_out/$TAG/sq1/run_counter_collection.csv > gpurun_out/$TAG/sq1.txt
 python3 - > gpurun_out/$TAG/sq2.txt <<PY

@@ -120,9 +120,10 @@ static int deflate_raw_pipelined(DeviceCtx *c, const uint8_t *in, size_t n, int 
   ZT_TRY(scratch(c, 1, pb * np, &d_out));
   const size_t ss = deflate_scratch_bytes(c, piece);
   ZT_TRY(scratch(c, 3, ss, &d_scr));
-  uint8_t *h = host_out(pb * np, true);
-  if (!h) return set_error(ZT_E_NOMEM, "host allocation failed");
-  size_t total = 0;
+  PipeOut po;
+  po.base = host_out(pb * np, true);
+  po.cap = pb * np;
+  if (!po.base) return set_error(ZT_E_NOMEM, "host allocation failed");
   const int rc = pipeline_h2d_d2h(
       c, np,
       [&](size_t i) {
@@ -137,13 +138,14 @@ static int deflate_raw_pipelined(DeviceCtx *c, const uint8_t *in, size_t n, int 
         *d_res = d_o;
         return ZT_OK;
       },
-      h, pb * np, &total);
+      po);
   if (rc) {
-    zt_free(h);
+    host_discard(po.base);
     return rc;
   }
-  *out = h;  // (its pages past the stream were never touched)
-  *out_len = total;
+  host_out_used(po.base, po.total);  // (zt_free registers the stream's pages, not the bound's)
+  *out = po.base;
+  *out_len = po.total;
   return ZT_OK;
 }
 

@@ -393,12 +393,15 @@ int inflate_dev_member(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t index
 // decoded and piece i - 1's bytes come back (pipeline_h2d_d2h).  A non-final
 // piece gets an empty final stored block (01 00 00 FF FF) after it on the
 // device and is decoded as a stream of its own: it must end exactly there,
-// which certifies that the cut is a real block boundary (a decode from a true
-// block start is deterministic -- reaching the appended block's end any
-// other way is impossible without consuming real block ends); a piece whose
+// and a unit of its segment chain must start at the cut.  The second is the
+// certificate that the cut is a real block boundary: the piece's decode
+// starts at a true block start (induction from the stream start), so a
+// block boundary exactly at the cut is the whole stream's boundary too --
+// ending on the appended block alone is not (a crafted Huffman block can
+// decode those five bytes as codes ending in EOB).  A piece whose
 // matches reach behind its start fails in the segment decoder.  Any failure
-// -- no marker, a piece the segment path cannot decode, an output past the
-// host bound -- returns 1 and the caller decodes the whole stream in one call
+// -- no marker, a piece the segment path cannot decode or certify --
+// returns 1 and the caller decodes the whole stream in one call
 // (tests/test_gpu_api_pipeline.py: identical output and end position).
 static constexpr size_t kInfPipeMin = 32u << 20;
 static constexpr size_t kInfPiece = 64u << 20;
@@ -424,16 +427,22 @@ static int inflate_raw_pipelined(DeviceCtx *c, const uint8_t *in, size_t n, size
   cut.push_back(n);
   const size_t np = cut.size() - 1;
   if (np < 2) return 1;
-  void *d_in, *d_out;
+  void *d_in;
   ZT_TRY(scratch(c, 0, m + 64 * np + 256, &d_in));
-  // outputs of up to 4x the input (the host bound below); past it: one call
-  const size_t cap = std::max<size_t>(4 * m, 64u << 20);
-  ZT_TRY(scratch(c, 22, cap, &d_out));
-  uint8_t *h = host_out(cap, true);  // (pages past the output are never touched)
-  if (!h) return set_error(ZT_E_NOMEM, "host allocation failed");
+  // Results go to a ring of kRing device buffers (scratch slots 22..24):
+  // piece i decodes into slot 22 + i % kRing once piece i - kRing's bytes have
+  // left the device.  A slot is sized 4x its piece's input, or from piece 0's
+  // output ratio when that is higher, and grown to what a piece reports it
+  // needs (one more decode of that piece); the host output starts at piece 0's
+  // ratio x the stream and grows the same way (pipeline_h2d_d2h), so a stream
+  // of any ratio stays pipelined.
+  constexpr size_t kRing = 3;
   auto d_piece = [&](size_t i) { return (uint8_t *)d_in + (cut[i] - index) + 64 * i; };
-  size_t off = 0, eip_last = 0;
-  size_t total = 0;
+  double ratio0 = 0;  // output bytes per input byte of piece 0
+  size_t eip_last = 0;
+  PipeOut po;
+  po.ring = kRing;
+  po.cap_fn = [&] { return (size_t)(ratio0 * 1.25 * (double)m) + (16u << 20); };
   const int rc = pipeline_h2d_d2h(
       c, np, [&](size_t i) { return PipePiece{in + cut[i], d_piece(i), cut[i + 1] - cut[i]}; },
       [&](size_t i, const void **d_res, size_t *n_res) -> int {
@@ -441,31 +450,42 @@ static int inflate_raw_pipelined(DeviceCtx *c, const uint8_t *in, size_t n, size
         const bool last = i + 1 == np;
         if (!last) ZT_HIP(hipMemcpyAsync(d_piece(i) + len, kFinal, sizeof kFinal, hipMemcpyHostToDevice, c->stream));
         const size_t pn = last ? len : len + sizeof kFinal;
-        uint8_t *d_o = (uint8_t *)d_out + off;
-        size_t ol = 0, eip = 0;
-        // the piece's output capacity: 4x its input first (the device chain's
-        // descriptors are sized from it), everything left if that is short
-        int seg = inflate_segments_dev(c, d_piece(i), pn, 0, &d_o, std::min(cap - off, 4 * pn + (1u << 20)), &ol,
-                                       &eip, c->stream);
-        if (seg < 0 && 4 * pn + (1u << 20) < cap - off)
-          seg = inflate_segments_dev(c, d_piece(i), pn, 0, &d_o, cap - off, &ol, &eip, c->stream);
-        // (no sync points in the piece: the speculative general decoder)
-        if (seg >= 1) seg = inflate_general_dev(c, d_piece(i), pn, 0, &d_o, cap - off, &ol, &eip, c->stream);
-        if (seg != 0) return seg < 0 ? seg : set_error(ZT_E_INTERNAL, "pipelined inflate: piece not decoded");
-        if (!last && eip != pn) return set_error(ZT_E_INTERNAL, "pipelined inflate: a cut is not a block boundary");
-        eip_last = eip;
-        *d_res = d_o;
-        *n_res = ol;
-        off += ol;
-        return ZT_OK;
+        const int slot = 22 + (int)(i % kRing);
+        size_t want = 4 * pn + (1u << 20);
+        if (i > 0) want = std::max(want, (size_t)(ratio0 * 1.25 * (double)pn) + (1u << 20));
+        for (int attempt = 0; attempt < 2; ++attempt) {
+          void *p;
+          ZT_TRY(scratch(c, slot, want, &p));
+          uint8_t *d_o = static_cast<uint8_t *>(p);
+          const size_t ocap = c->buf_size[slot];
+          size_t ol = 0, eip = 0;
+          // a non-final piece must have a block boundary right before its
+          // appended final block (the cut) -- and must end on that block
+          int seg = inflate_segments_dev(c, d_piece(i), pn, 0, &d_o, ocap, &ol, &eip, c->stream, last ? ~0ull : len);
+          if (seg < 0 && ol > ocap && attempt == 0) {  // more output than the slot: grow it, decode again
+            want = ol + (1u << 20);
+            continue;
+          }
+          // (no sync points in the last piece: the speculative general decoder)
+          if (seg >= 1 && last) seg = inflate_general_dev(c, d_piece(i), pn, 0, &d_o, ocap, &ol, &eip, c->stream);
+          if (seg != 0) return seg < 0 ? seg : set_error(ZT_E_INTERNAL, "pipelined inflate: piece not decoded");
+          if (!last && eip != pn) return set_error(ZT_E_INTERNAL, "pipelined inflate: a cut is not a block boundary");
+          if (i == 0) ratio0 = (double)ol / (double)pn;
+          eip_last = eip;
+          *d_res = d_o;
+          *n_res = ol;
+          return ZT_OK;
+        }
+        return set_error(ZT_E_INTERNAL, "pipelined inflate: piece output did not settle");
       },
-      h, cap, &total);
-  if (rc) {
-    zt_free(h);
+      po);
+  if (rc) {  // (every copy has finished: the buffer can go)
+    host_discard(po.base);
     return 1;
   }
-  *out = h;
-  *out_len = total;
+  host_out_used(po.base, po.total);
+  *out = po.base;
+  *out_len = po.total;
   if (end_ip) *end_ip = cut[np - 1] + eip_last;
   return ZT_OK;
 }

@@ -497,8 +497,15 @@ static double it_now() {
     if (on_) fprintf(stderr, "[inflate] %-24s %9.3f ms\n", label, it_now()); \
   } while (0)
 
+// a unit of the chain starts at byte `pos` (the device chain: every unit is
+// on it); flag[0] |= 1 then
+__global__ void unit_starts_at(const TokJob *__restrict__ jobs, uint32_t units, uint64_t pos, uint32_t *flag) {
+  for (uint32_t u = blockIdx.x * blockDim.x + threadIdx.x; u < units; u += gridDim.x * blockDim.x)
+    if (jobs[u].start == pos) atomicOr(flag, 1u);
+}
+
 int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t index, uint8_t **d_out_io,
-                         size_t out_cap, size_t *out_len, size_t *end_ip, hipStream_t s) {
+                         size_t out_cap, size_t *out_len, size_t *end_ip, hipStream_t s, uint64_t boundary) {
   IT("start");
   if (n < index + (1u << 14)) return 1;  // small: one wave is as fast
   // 1. sync points
@@ -641,7 +648,7 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
     void *d_chain, *d_desc;
     const size_t chain_bytes = align256(units * sizeof(ChainUnit)), seg_bytes = align256(max_seg * sizeof(SegJob));
     const size_t ust_bytes = align256(units * 4), st_bytes = align256(max_seg * 4);
-    ZT_TRY(scratch(c, 7, chain_bytes + seg_bytes + ust_bytes + st_bytes + 256, &d_chain));
+    ZT_TRY(scratch(c, 7, chain_bytes + seg_bytes + ust_bytes + st_bytes + 512, &d_chain));
     if (scratch(c, 3, desc_cap * 2, &d_desc) != ZT_OK) {
       (void)hipGetLastError();  // (the failed allocation's sticky error)
       goto host_walk;
@@ -652,6 +659,13 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
     int32_t *d_ust = reinterpret_cast<int32_t *>(cb + chain_bytes + seg_bytes);
     int32_t *d_st = reinterpret_cast<int32_t *>(cb + chain_bytes + seg_bytes + ust_bytes);
     ChainInfo *d_info = reinterpret_cast<ChainInfo *>(cb + chain_bytes + seg_bytes + ust_bytes + st_bytes);
+    uint32_t *d_bflag = reinterpret_cast<uint32_t *>(d_info + 1);
+    if (boundary != ~0ull) {
+      ZT_HIP(hipMemsetAsync(d_bflag, 0, 4, s));
+      unit_starts_at<<<(uint32_t)std::min<size_t>(64, (units + 255) / 256), 256, 0, s>>>(d_jobs, (uint32_t)units,
+                                                                                        boundary, d_bflag);
+      ZT_HIP(hipGetLastError());
+    }
     chain_kernel<<<1, CH_T, 0, s>>>(d_res, d_restart, d_off, (uint32_t)units, out_cap, desc_cap, max_seg, d_cu, d_sj,
                                     d_info);
     ZT_HIP(hipGetLastError());
@@ -673,11 +687,13 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
     ZT_TRY(timing_end(c, s, 2));
     // back in one copy: the chain summary and every status
     uint8_t *hb = pin + meta_a;
-    ZT_HIP(hipMemcpyAsync(hb, d_ust, ust_bytes + st_bytes + sizeof(ChainInfo), hipMemcpyDeviceToHost, s));
+    ZT_HIP(hipMemcpyAsync(hb, d_ust, ust_bytes + st_bytes + sizeof(ChainInfo) + 4, hipMemcpyDeviceToHost, s));
     ZT_HIP(hipStreamSynchronize(s));
     IT("resolved (device chain)");
     const ChainInfo info = *reinterpret_cast<const ChainInfo *>(hb + ust_bytes + st_bytes);
     if (info.ok) {
+      if (boundary != ~0ull && !*reinterpret_cast<const uint32_t *>(hb + ust_bytes + st_bytes + sizeof(ChainInfo)))
+        FALLBACK("no unit of the chain starts at the boundary %llu\n", (unsigned long long)boundary);
       ZT_TRY(timing_collect(c, &c->times.inflate_ms, &c->times.inflate_launches, 2));
       ZT_TRY(timing_collect(c, &c->times.inflate_tok_ms, &c->times.inflate_toks, 3));
       const int32_t *h_ust = reinterpret_cast<const int32_t *>(hb);
@@ -730,6 +746,7 @@ host_walk:
     }
   }
   // 3. the chain from the stream start, cut into segments at restart markers
+  std::vector<size_t> chained;  // (units on the chain, for the boundary check)
   std::vector<ChainUnit> chain;
   std::vector<SegJob> segs;
   uint64_t total = 0, seg_start = 0, desc_total = 0, desc_seg = 0;
@@ -760,6 +777,7 @@ host_walk:
     }
     chain.push_back(ChainUnit{tok_off[u], total, seg_start, desc_seg + (total - seg_start), r.ntok,
                               (uint32_t)r.out_len});
+    chained.push_back(u);
     segs.back().count++;
     total += r.out_len;
     desc_total = desc_seg + (total - seg_start);
@@ -779,6 +797,14 @@ host_walk:
     }
     for (uint32_t k = 0; k < sj.count && !direct; ++k) chain[sj.first + k].ntok &= ~0x40000000u;
     if (direct) sj.count |= 0x80000000u;
+  }
+  if (boundary != ~0ull) {
+    std::vector<TokJob> hj(units);
+    ZT_HIP(hipMemcpyAsync(hj.data(), d_jobs, units * sizeof(TokJob), hipMemcpyDeviceToHost, s));
+    ZT_HIP(hipStreamSynchronize(s));
+    bool at = false;
+    for (size_t k : chained) at = at || hj[k].start == boundary;
+    if (!at) FALLBACK("no unit of the chain starts at the boundary %llu\n", (unsigned long long)boundary);
   }
   *out_len = total;
   *end_ip = (res[u].end_bits + 7) >> 3;
@@ -803,6 +829,7 @@ host_walk:
     d_out = static_cast<uint8_t *>(p);
     *d_out_io = d_out;
   } else if (total > out_cap) {
+    *out_len = total;  // (the bytes needed)
     return set_error(ZT_E_ARG, "output capacity too small");
   }
   // 4. expand (one wave per unit) and copy (one wave per segment)

@@ -126,7 +126,11 @@ int scratch(DeviceCtx *c, int slot, size_t bytes, void **ptr) {
       c->buf_size[slot] = 0;
     }
     size_t sz = bytes + bytes / 4;
-    ZT_HIP(hipMalloc(&c->d_buf[slot], sz));
+    if (const hipError_t e = hipMalloc(&c->d_buf[slot], sz)) {
+      c->d_buf[slot] = nullptr;
+      (void)hipGetLastError();  // (a caller that falls back must not see it at its next launch check)
+      return hip_fail(e, "hipMalloc (scratch)");
+    }
     c->buf_size[slot] = sz;
   }
   *ptr = c->d_buf[slot];
@@ -157,9 +161,11 @@ static uint8_t *host_alloc(size_t n) {
 struct PoolBuf {
   uint8_t *p;
   size_t cap;
+  size_t len;      // bytes the current use returns (host_out_used; default: the request)
+  size_t hi;       // the most any use returned: the pages ever touched
+  size_t reg_len;  // registered prefix (hipHostRegister of [p, p + reg_len)), 0: none
   bool used;
-  bool reg;      // registered with HIP
-  bool reg_bad;  // registration failed once: not tried again
+  bool reg_bad;    // registration failed once: not tried again
 };
 static std::mutex g_pool_mu;
 static std::vector<PoolBuf> g_pool;
@@ -172,17 +178,20 @@ static size_t pool_limit() {
   return v;
 }
 
+// resident bytes of a free pool buffer: the pages its uses touched
+static size_t pool_resident(const PoolBuf &e) { return std::max(e.hi, e.reg_len); }
+
 // free pool buffers beyond the bound, largest first (g_pool_mu held)
 static void pool_trim(size_t limit) {
   for (;;) {
     size_t free_bytes = 0, big = SIZE_MAX;
     for (size_t i = 0; i < g_pool.size(); ++i)
       if (!g_pool[i].used) {
-        free_bytes += g_pool[i].cap;
-        if (big == SIZE_MAX || g_pool[i].cap > g_pool[big].cap) big = i;
+        free_bytes += pool_resident(g_pool[i]);
+        if (big == SIZE_MAX || pool_resident(g_pool[i]) > pool_resident(g_pool[big])) big = i;
       }
-    if (free_bytes <= limit || big == SIZE_MAX) return;
-    if (g_pool[big].reg) (void)hipHostUnregister(g_pool[big].p);
+    if (big == SIZE_MAX || (limit && free_bytes <= limit)) return;  // (limit 0: all of them)
+    if (g_pool[big].reg_len) (void)hipHostUnregister(g_pool[big].p);
     free(g_pool[big].p);
     g_pool.erase(g_pool.begin() + (long)big);
   }
@@ -200,42 +209,81 @@ uint8_t *host_out(size_t n, bool pool) {
     }
     if (best != SIZE_MAX) {
       g_pool[best].used = true;
+      g_pool[best].len = n;
       return g_pool[best].p;
     }
   }
   uint8_t *p = host_alloc(n);
   if (!p) return nullptr;
   std::lock_guard<std::mutex> lk(g_pool_mu);
-  g_pool.push_back(PoolBuf{p, n, true, false, false});
+  g_pool.push_back(PoolBuf{p, n, n, 0, 0, true, false});
   return p;
 }
 
-// a pool buffer back to the pool (false: p is not one)
-static bool pool_release(void *p) {
+void host_out_used(void *p, size_t n) {
   std::lock_guard<std::mutex> lk(g_pool_mu);
   for (PoolBuf &e : g_pool)
-    if (e.p == p && e.used) {
-      e.used = false;
-      if (!e.reg && !e.reg_bad) {
-        e.reg = hipHostRegister(e.p, e.cap, hipHostRegisterPortable) == hipSuccess;
-        e.reg_bad = !e.reg;
-        if (!e.reg) (void)hipGetLastError();
+    if (e.p == p && e.used) e.len = std::min(n, e.cap);
+}
+
+// A pool buffer back to the pool (false: p is not one).  The pages its uses
+// returned are registered with HIP on the way in -- not its whole capacity
+// (a pipelined inflate's buffer is sized for several times its input), and
+// outside g_pool_mu (~25 ms per GiB): the buffer stays `used` meanwhile, so
+// no other thread takes or trims it, and other threads' host_out / zt_free
+// go on.
+static bool pool_release(void *p) {
+  std::unique_lock<std::mutex> lk(g_pool_mu);
+  PoolBuf *e = nullptr;
+  for (PoolBuf &x : g_pool)
+    if (x.p == p && x.used) e = &x;
+  if (!e) return false;
+  e->hi = std::max(e->hi, e->len);
+  const size_t want = std::min(e->cap, (e->hi + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1));
+  if (!e->reg_bad && want > e->reg_len) {
+    uint8_t *bp = e->p;
+    const size_t old = e->reg_len;
+    lk.unlock();
+    if (old) (void)hipHostUnregister(bp);
+    const bool ok = hipHostRegister(bp, want, hipHostRegisterPortable) == hipSuccess;
+    if (!ok) (void)hipGetLastError();
+    lk.lock();
+    for (PoolBuf &x : g_pool)
+      if (x.p == bp) {
+        x.reg_len = ok ? want : 0;
+        x.reg_bad = !ok;
+        x.used = false;
       }
-      pool_trim(pool_limit());
-      return true;
-    }
-  return false;
+  } else {
+    e->used = false;
+  }
+  pool_trim(pool_limit());
+  return true;
 }
 
 void host_release(void *p) {
   if (!pool_release(p)) free(p);
 }
 
+void host_discard(void *p) {
+  if (!p) return;
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    for (size_t i = 0; i < g_pool.size(); ++i)
+      if (g_pool[i].p == p && g_pool[i].used) {
+        if (g_pool[i].reg_len) (void)hipHostUnregister(p);
+        g_pool.erase(g_pool.begin() + (long)i);
+        break;
+      }
+  }
+  free(p);
+}
+
 bool host_direct(const void *p, size_t n) {
   const uint8_t *q = static_cast<const uint8_t *>(p);
   std::lock_guard<std::mutex> lk(g_pool_mu);
   for (const PoolBuf &e : g_pool)
-    if (e.used && e.reg && q >= e.p && q + n <= e.p + e.cap) return true;
+    if (e.used && e.reg_len && q >= e.p && q + n <= e.p + e.reg_len) return true;
   return false;
 }
 
@@ -283,7 +331,11 @@ int pinned(DeviceCtx *c, size_t bytes, void **ptr, int slot) {
       c->pinned_size[slot] = 0;
     }
     size_t sz = bytes + bytes / 4;
-    ZT_HIP(hipHostMalloc(&c->h_pinned[slot], sz, hipHostMallocDefault));
+    if (const hipError_t e = hipHostMalloc(&c->h_pinned[slot], sz, hipHostMallocDefault)) {
+      c->h_pinned[slot] = nullptr;
+      (void)hipGetLastError();
+      return hip_fail(e, "hipHostMalloc (staging)");
+    }
     c->pinned_size[slot] = sz;
   }
   *ptr = c->h_pinned[slot];
@@ -371,10 +423,11 @@ int download(DeviceCtx *c, void *h_dst, const void *d_src, size_t n, hipStream_t
 // pipeline_h2d_d2h (zt_internal.h).  Each stage runs in order over the
 // pieces; the stages hand pieces on through counters under one mutex, and a
 // failing stage stops the others (its error text is re-raised on the
-// caller's thread, where zt_last_error_message() reads it).
+// caller's thread, where zt_last_error_message() reads it).  Every stream the
+// pipeline used is drained before it returns, on error paths too: the caller
+// may free the output (or the input) as soon as it has the status.
 int pipeline_h2d_d2h(DeviceCtx *c, size_t np, const std::function<PipePiece(size_t)> &input,
-                     const std::function<int(size_t, const void **d_res, size_t *n_res)> &compute, uint8_t *out_base,
-                     size_t out_cap, size_t *out_total) {
+                     const std::function<int(size_t, const void **d_res, size_t *n_res)> &compute, PipeOut &out) {
   if (!c->up) ZT_HIP(hipStreamCreateWithFlags(&c->up, hipStreamNonBlocking));
   if (!c->dn) ZT_HIP(hipStreamCreateWithFlags(&c->dn, hipStreamNonBlocking));
   uint8_t *stage[4];
@@ -384,19 +437,23 @@ int pipeline_h2d_d2h(DeviceCtx *c, size_t np, const std::function<PipePiece(size
     stage[k] = static_cast<uint8_t *>(p);
     if (!c->xfer_ev[k]) ZT_HIP(hipEventCreateWithFlags(&c->xfer_ev[k], hipEventDisableTiming));
   }
-  std::vector<hipEvent_t> landed(np, nullptr);
+  std::vector<hipEvent_t> landed(np, nullptr), drained(np, nullptr);
   struct EvFree {
     std::vector<hipEvent_t> &v;
     ~EvFree() {
       for (auto e : v)
         if (e) (void)hipEventDestroy(e);
     }
-  } ev_free{landed};
+  } ev_free{landed}, ev_free2{drained};
   for (auto &e : landed) ZT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  if (out.ring)
+    for (auto &e : drained) ZT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
 
   std::mutex mu;
   std::condition_variable cv;
-  size_t uploaded = 0, computed = 0;  // pieces whose upload is enqueued / whose result is on the device
+  // pieces whose upload is enqueued / whose result is on the device / whose
+  // result's copy back is enqueued (with `drained` recorded behind it)
+  size_t uploaded = 0, computed = 0, downloaded = 0;
   std::vector<const void *> res(np, nullptr);
   std::vector<size_t> res_n(np, 0);
   int err = 0;
@@ -435,12 +492,12 @@ int pipeline_h2d_d2h(DeviceCtx *c, size_t np, const std::function<PipePiece(size
       uploaded = i + 1;
       cv.notify_all();
     }
-    ZT_HIP(hipStreamSynchronize(c->up));  // the staging chunks are reused by the next call
     return ZT_OK;
   };
-  // stage 3: device -> pinned chunk (DMA on c->dn) -> host (host threads)
-  size_t total = 0;
-  const bool direct = host_direct(out_base, out_cap);  // a registered pool buffer: DMA straight into it
+  // stage 3: device -> host: straight into a registered pool buffer (DMA on
+  // c->dn), else device -> pinned chunk (DMA on c->dn) -> host (host threads)
+  uint8_t *base = out.base;
+  size_t cap = out.cap, total = 0;
   auto dn_stage = [&]() -> int {
     ZT_HIP(hipSetDevice(dev));
     size_t k = 0;
@@ -451,32 +508,48 @@ int pipeline_h2d_d2h(DeviceCtx *c, size_t np, const std::function<PipePiece(size
         if (err) return ZT_OK;
       }
       const size_t n = res_n[i];
-      if (total + n > out_cap) return set_error(ZT_E_ARG, "pipeline output larger than its bound");
-      if (direct) {
-        if (n) ZT_HIP(hipMemcpyAsync(out_base + total, res[i], n, hipMemcpyDeviceToHost, c->dn));
-        total += n;
-        continue;
+      if (!base) {  // (the output's size estimate may look at piece 0's result)
+        cap = std::max(out.cap_fn ? out.cap_fn() : (size_t)0, n);
+        base = host_out(cap, true);
+        if (!base) return set_error(ZT_E_NOMEM, "host allocation failed");
       }
-      // chunks of this piece: issue k + 1 before copying k out of its staging buffer
-      const size_t nch = (n + kXferChunk - 1) / kXferChunk;
-      auto issue = [&](size_t j) -> int {
-        const size_t off = j * kXferChunk, len = std::min(kXferChunk, n - off);
-        ZT_HIP(hipMemcpyAsync(stage[2 + ((k + j) & 1)], (const uint8_t *)res[i] + off, len, hipMemcpyDeviceToHost,
-                              c->dn));
-        ZT_HIP(hipEventRecord(c->xfer_ev[2 + ((k + j) & 1)], c->dn));
-        return ZT_OK;
-      };
-      if (nch) ZT_TRY(issue(0));
-      for (size_t j = 0; j < nch; ++j) {
-        if (j + 1 < nch) ZT_TRY(issue(j + 1));
-        ZT_HIP(hipEventSynchronize(c->xfer_ev[2 + ((k + j) & 1)]));
-        const size_t off = j * kXferChunk, len = std::min(kXferChunk, n - off);
-        host_copy(out_base + total + off, stage[2 + ((k + j) & 1)], len);
+      if (total + n > cap) {  // a larger buffer: the bytes so far move over
+        const size_t ncap = std::max(2 * cap, total + n + (total + n) / 4);
+        uint8_t *nb = host_out(ncap, true);
+        if (!nb) return set_error(ZT_E_NOMEM, "host allocation failed");
+        ZT_HIP(hipStreamSynchronize(c->dn));
+        host_copy(nb, base, total);
+        host_discard(base);
+        base = nb;
+        cap = ncap;
       }
-      k += nch;
+      if (host_direct(base + total, n)) {
+        if (n) ZT_HIP(hipMemcpyAsync(base + total, res[i], n, hipMemcpyDeviceToHost, c->dn));
+      } else {
+        // chunks of this piece: issue k + 1 before copying k out of its staging buffer
+        const size_t nch = (n + kXferChunk - 1) / kXferChunk;
+        auto issue = [&](size_t j) -> int {
+          const size_t off = j * kXferChunk, len = std::min(kXferChunk, n - off);
+          ZT_HIP(hipMemcpyAsync(stage[2 + ((k + j) & 1)], (const uint8_t *)res[i] + off, len, hipMemcpyDeviceToHost,
+                                c->dn));
+          ZT_HIP(hipEventRecord(c->xfer_ev[2 + ((k + j) & 1)], c->dn));
+          return ZT_OK;
+        };
+        if (nch) ZT_TRY(issue(0));
+        for (size_t j = 0; j < nch; ++j) {
+          if (j + 1 < nch) ZT_TRY(issue(j + 1));
+          ZT_HIP(hipEventSynchronize(c->xfer_ev[2 + ((k + j) & 1)]));
+          const size_t off = j * kXferChunk, len = std::min(kXferChunk, n - off);
+          host_copy(base + total + off, stage[2 + ((k + j) & 1)], len);
+        }
+        k += nch;
+      }
       total += n;
+      if (out.ring) ZT_HIP(hipEventRecord(drained[i], c->dn));
+      std::lock_guard<std::mutex> lk(mu);
+      downloaded = i + 1;
+      cv.notify_all();
     }
-    if (direct) ZT_HIP(hipStreamSynchronize(c->dn));
     return ZT_OK;
   };
   std::thread tu([&] {
@@ -485,15 +558,18 @@ int pipeline_h2d_d2h(DeviceCtx *c, size_t np, const std::function<PipePiece(size
   std::thread td([&] {
     if (int rc = dn_stage()) fail(rc);
   });
-  // stage 2 on the caller's thread: compute(i) after piece i has landed
+  // stage 2 on the caller's thread: compute(i) after piece i has landed (and,
+  // with a ring, after piece i - ring's result has left the device)
   for (size_t i = 0; i < np; ++i) {
     {
       std::unique_lock<std::mutex> lk(mu);
-      cv.wait(lk, [&] { return uploaded > i || err; });
+      cv.wait(lk, [&] { return (uploaded > i && (!out.ring || i < out.ring || downloaded > i - out.ring)) || err; });
       if (err) break;
     }
     int rc = hipStreamWaitEvent(c->stream, landed[i], 0) == hipSuccess ? ZT_OK
                                                                        : set_error(ZT_E_HIP, "hipStreamWaitEvent");
+    if (!rc && out.ring && i >= out.ring && hipStreamWaitEvent(c->stream, drained[i - out.ring], 0) != hipSuccess)
+      rc = set_error(ZT_E_HIP, "hipStreamWaitEvent");
     const void *d = nullptr;
     size_t m = 0;
     if (!rc) rc = compute(i, &d, &m);
@@ -509,8 +585,20 @@ int pipeline_h2d_d2h(DeviceCtx *c, size_t np, const std::function<PipePiece(size
   }
   tu.join();
   td.join();
-  if (err) return set_error(err, err_msg);
-  *out_total = total;
+  // nothing may still be copying into the output or out of the input when
+  // the caller gets it back (error paths: zt_free / reuse right after)
+  const hipError_t e1 = hipStreamSynchronize(c->up), e2 = hipStreamSynchronize(c->dn),
+                   e3 = hipStreamSynchronize(c->stream);
+  out.base = base;
+  out.cap = cap;
+  out.total = total;
+  if (err) {
+    (void)hipGetLastError();
+    return set_error(err, err_msg);
+  }
+  if (e1 != hipSuccess) return hip_fail(e1, "pipeline upload stream");
+  if (e2 != hipSuccess) return hip_fail(e2, "pipeline download stream");
+  if (e3 != hipSuccess) return hip_fail(e3, "pipeline compute stream");
   return ZT_OK;
 }
 

@@ -52,10 +52,10 @@ struct DeviceCtx {
   uint32_t *d_crc_shift = nullptr;  // checksum.hip merge constants (crc_shift_tables)
   CkAcc *d_ck_acc = nullptr;        // checksum merge accumulators (zeroed once, left zeroed by every call)
   // scratch
-  static constexpr int kSlots = 23;
+  static constexpr int kSlots = 26;
   void *d_buf[kSlots] = {};  // slot 8: checksum segment partials; 10-17: general inflate (inflate_gen.hip);
                              // 20: segment inflate's sync-point sort (inflate_seg.hip); 21: stored runs;
-                             // 22: pipelined host inflate's output (inflate_api.cpp)
+                             // 22-24: pipelined host inflate's output ring (inflate_api.cpp)
   size_t buf_size[kSlots] = {};
   // second stream: checksums run beside the deflate pipeline in the containers
   hipStream_t aux = nullptr;
@@ -91,6 +91,11 @@ int pinned(DeviceCtx *c, size_t bytes, void **ptr, int slot = 0);
 // by DMA without staging.
 uint8_t *host_out(size_t n, bool pool = false);
 void host_release(void *p);
+// host_out_used: the bytes a pooled output actually returns (what zt_free
+// registers), when less than requested; host_discard: an output never handed
+// out (an error path) freed outright instead of pooled
+void host_out_used(void *p, size_t n);
+void host_discard(void *p);
 bool host_direct(const void *p, size_t n);
 // One host allocation for `items` batch outputs (pointers inside it, each
 // released by zt_free; reserve >= 1 byte per item so every pointer is
@@ -211,9 +216,14 @@ struct InfResult {
 
 // segment-parallel inflate (restart markers written by deflate); returns 1 when
 // the stream has no usable segments (caller decodes it with one wave)
-// (*d_out_io null: the output goes to scratch slot 1, returned in *d_out_io)
+// (*d_out_io null: the output goes to scratch slot 1, returned in *d_out_io;
+// a caller-owned output too small for the stream: ZT_E_ARG with *out_len = the
+// bytes it needs).  boundary (a byte position, or ~0: none): the decode must
+// have a block boundary there -- a unit of the chain starts at it -- or the
+// call returns 1 (the pipelined host inflate's certificate that a cut is a
+// real block boundary of the whole stream)
 int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t index, uint8_t **d_out_io,
-                         size_t out_cap, size_t *out_len, size_t *end_ip, hipStream_t s);
+                         size_t out_cap, size_t *out_len, size_t *end_ip, hipStream_t s, uint64_t boundary = ~0ull);
 
 
 // ---- two-phase token inflate (inflate_tok.hip) ----------------------------------
@@ -360,16 +370,29 @@ int download(DeviceCtx *c, void *h_dst, const void *d_src, size_t n, hipStream_t
 // i + 1 crosses PCIe to the device (pinned chunks, stream c->up, one host
 // thread) while compute(i) runs on the caller's thread (after piece i's upload
 // has landed; it returns the device bytes of its result) and piece i - 1's
-// result comes back (pinned chunks, stream c->dn, one host thread) to
-// out_base + the sum of the earlier results' lengths (out_cap bytes in all).
+// result comes back (stream c->dn, one host thread: straight into a
+// registered pool buffer by DMA, else through pinned chunks) to out.base +
+// the sum of the earlier results' lengths.
 struct PipePiece {
   const void *h_src;  // host bytes of piece i
   void *d_dst;        // where they go on the device
   size_t n;
 };
+struct PipeOut {
+  // host output of `cap` bytes; null: the download stage takes a pooled
+  // host_out(cap_fn()) once piece 0 is computed (cap_fn may look at it).  A
+  // result that does not fit moves the bytes so far into a larger buffer.  On
+  // return -- error or not, every copy finished -- `base` is the caller's.
+  uint8_t *base = nullptr;
+  size_t cap = 0;
+  std::function<size_t()> cap_fn;
+  // > 0: compute(i) starts only after piece i - ring's result has left the
+  // device (device result buffers reused round robin)
+  size_t ring = 0;
+  size_t total = 0;  // out: bytes written
+};
 int pipeline_h2d_d2h(DeviceCtx *c, size_t np, const std::function<PipePiece(size_t)> &input,
-                     const std::function<int(size_t, const void **d_res, size_t *n_res)> &compute, uint8_t *out_base,
-                     size_t out_cap, size_t *out_total);
+                     const std::function<int(size_t, const void **d_res, size_t *n_res)> &compute, PipeOut &out);
 int inflate_error(int status, int detail);
 
 }  // namespace zt

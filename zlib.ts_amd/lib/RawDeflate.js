@@ -39,8 +39,13 @@ export class RawDeflate {
             throw e;
         }
         const start = this.op;
+        if (start === 0) {  // no caller prefix: the library's buffer itself (no copy)
+            this.output = stream;
+            this.op = stream.length;
+            return stream;
+        }
         const out = new Uint8Array(start + stream.length);
-        if (start) out.set(this.output.subarray(0, Math.min(start, this.output.length)));
+        out.set(this.output.subarray(0, Math.min(start, this.output.length)));
         out.set(stream, start);
         this.output = out;
         this.op = out.length;

@@ -1,7 +1,8 @@
 // zt_napi.cc -- N-API addon: the thin binding between the JS facade
 // (zlib.ts_amd/lib/*.js, the reference's RawDeflate / RawInflate / CRC32 /
 // Adler32 surface) and libzt.so's C-ABI (include/zt.h).  Uint8Array memory is
-// passed zero-copy; results come back as new Uint8Arrays.  Every call runs on
+// passed zero-copy; results come back as Uint8Arrays over the library's own
+// output buffers (no copy, released by zt_free on collection).  Every call runs on
 // the GPU; errors carry libzt's status code and message (the JS facade maps
 // them onto the reference's thrown values).
 #include <node_api.h>
@@ -68,13 +69,33 @@ uint32_t get_u32(napi_env env, napi_value v, uint32_t dflt) {
   return x;
 }
 
-// copies a libzt-allocated result into a new Uint8Array and frees it
+// A libzt-allocated result handed to JS without a copy: an external
+// ArrayBuffer over the library's buffer, released by zt_free when the GC
+// collects it (large outputs then go back to libzt's host output pool,
+// registered for DMA, and the next call of a similar size reuses them).  The
+// bytes are reported to V8 as external memory so that a loop of large calls
+// triggers collections.
+void release_result(napi_env env, void *data, void *hint) {
+  zt_free(data);
+  int64_t adj = 0;
+  napi_adjust_external_memory(env, -(int64_t)(uintptr_t)hint, &adj);
+}
+
 napi_value new_u8(napi_env env, uint8_t *buf, size_t n) {
-  void *data = nullptr;
   napi_value ab, ta;
-  napi_create_arraybuffer(env, n, &data, &ab);
-  if (n) memcpy(data, buf, n);
-  zt_free(buf);
+  if (n == 0 || !buf) {
+    void *data = nullptr;
+    napi_create_arraybuffer(env, 0, &data, &ab);
+    zt_free(buf);
+  } else if (napi_create_external_arraybuffer(env, buf, n, release_result, (void *)(uintptr_t)n, &ab) == napi_ok) {
+    int64_t adj = 0;
+    napi_adjust_external_memory(env, (int64_t)n, &adj);
+  } else {  // (a runtime without external buffers: copy)
+    void *data = nullptr;
+    napi_create_arraybuffer(env, n, &data, &ab);
+    memcpy(data, buf, n);
+    zt_free(buf);
+  }
   napi_create_typedarray(env, napi_uint8_array, n, ab, 0, &ta);
   return ta;
 }
