@@ -43,3 +43,31 @@ def test_per_generator_ratio(gate_rows):
         r = sum(x[3] for x in gate_rows if x[0] == gen)
         print(gen, round(o / r, 4))
         assert o / r <= GATE, gen
+
+
+def test_adaptive_depth_engages_within_gate(oracle, gate_rows):
+    """Level 6 chooses each block's search depth from its first 4 KiB
+    (deflate.hip DeflateParams::adapt_depth): on the source-text and
+    structured windows some blocks walk fewer hops than max_chain -- the
+    streams differ from the fixed-depth ones (ZT_DF_ADAPT=0,0) -- and every
+    window, adaptive or not, stays within the gate.  Streams decode through
+    the reference's RawInflate restatement."""
+    import os
+
+    import ztamd
+
+    wins = windows(oracle)
+    gated = {label: (ours, ref) for _, label, ours, ref in gate_rows}
+    differ = 0
+    os.environ["ZT_DF_ADAPT"] = "0,0"
+    try:
+        for gen, label, data in wins:
+            if gen not in ("source", "structured"):
+                continue
+            fixed = ztamd.deflate_raw(data, level=6)
+            ours, ref = gated[label]
+            assert len(fixed) / ref <= GATE and ours / ref <= GATE, label
+            differ += len(fixed) != ours
+    finally:
+        del os.environ["ZT_DF_ADAPT"]
+    assert differ > 0, "no block took the shallower depth"

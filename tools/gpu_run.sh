@@ -15,11 +15,14 @@
 #   c1 / c2 / c4      rocprof kernel stats of C1 / C2 / C4    (cN_kernel_stats.csv)
 #   c4batch           C4 end to end                           (c4_batch.json)
 #   c4host            C4 host stages on 8 aliased devices     (c4_host_stages.json)
-#   api               host-API inflate time                   (api.log)
+#   api               host-API inflate time (appends)         (api.log)
+#   infprof           rocprof kernel stats of infgen          (infgen_kernel_stats.csv)
 #   infgen[:MiB]      foreign-stream inflate timing           (inflate_general_time.json)
 #   kinds             per-generator deflate / inflate times   (kinds.log)
 #   digest            stream digests (levels 6 / 1 / 9)       (digest.log)
 #   node              Node facade bench (tools/node_bench.mjs) (node.log)
+#   adapt:S1;S2;...   per-block depth sweep (ZT_DF_ADAPT settings) (adapt.log)
+#   regprobe          hipHostRegister vs pack of C4-sized buffers (regprobe.log)
 #   lib=PATH          later steps load libzt from PATH (ZT_LIB); lib= resets
 #   env=K=V           later steps see K=V
 set -e
@@ -57,12 +60,15 @@ for step in "$@"; do
     c4) prof c4 300 -- python3 $R/tools/c4_batch.py 10000 ;;
     c4batch) timeout -k 10 300 python3 tools/c4_batch.py 10000 $O/c4_batch.json > $O/c4.log 2>&1; tail -3 $O/c4.log | cut -c1-300 ;;
     c4host) ZT_ALIAS_DEVICES=8 timeout -k 10 600 python3 tools/c4_host_stages.py 10000 $O/c4_host_stages.json > $O/c4_host_stages.log 2>&1; tail -5 $O/c4_host_stages.log ;;
-    api) timeout -k 10 300 python3 tools/api_inflate_time.py > $O/api.log 2>&1; tail -1 $O/api.log ;;
+    api) timeout -k 10 300 python3 tools/api_inflate_time.py >> $O/api.log 2>&1; echo "${ZT_LIB:-HEAD} $(tail -1 $O/api.log)" ;;
+    infprof) prof infgen 600 -- python3 $R/tools/inflate_general_time.py 64 ;;
     infgen) timeout -k 10 600 python3 -u tools/inflate_general_time.py 64 $O/inflate_general_time.json > $O/infgen.log 2>&1; tail -1 $O/infgen.log | cut -c1-600 ;;
     infgen:*) timeout -k 10 600 python3 -u tools/inflate_general_time.py ${step#infgen:} $O/inflate_general_time.json > $O/infgen.log 2>&1; tail -1 $O/infgen.log | cut -c1-600 ;;
     kinds) timeout -k 10 300 python3 tools/kind_time.py > $O/kinds.log 2>&1; tail -8 $O/kinds.log ;;
     digest) DF_LEVELS=6,1,9 timeout -k 10 300 python3 tools/df_digest.py wordsalad structured mixed > $O/digest.log 2>&1; grep -E 'L6|L1|L9' $O/digest.log ;;
     node) timeout -k 10 300 node --expose-gc tools/node_bench.mjs > $O/node.log 2>&1; tail -1 $O/node.log ;;
+    adapt:*) IFS=';' read -ra A <<< "${step#adapt:}"; timeout -k 10 900 python3 -u tools/adapt_sweep.py "" "${A[@]}" > $O/adapt.log 2>&1; grep '^\[' $O/adapt.log ;;
+    regprobe) timeout -k 10 300 tools/micro/host_register_probe > $O/regprobe.log 2>&1; cat $O/regprobe.log ;;
     lib=) unset ZT_LIB ;;
     lib=*) export ZT_LIB=$R/${step#lib=} ;;
     env=*) export "${step#env=}" ;;

@@ -14,7 +14,10 @@
 import fs from 'fs';
 import { RawDeflate, RawInflate } from '../zlib.ts_amd/lib/index.js';
 
-const gc = typeof global.gc === 'function' ? global.gc : () => {};
+const gcRaw = typeof global.gc === 'function' ? global.gc : () => {};
+// a collection, then one event-loop turn: N-API runs the external buffers'
+// finalizers (zt_free) after the collection, not inside it
+const gc = () => { gcRaw(); return new Promise((r) => setImmediate(r)); };
 const now = () => Number(process.hrtime.bigint()) / 1e6;  // ms
 const median = (a) => a.slice().sort((x, y) => x - y)[a.length >> 1];
 const same = (a, b) => a.length === b.length &&
@@ -35,6 +38,7 @@ function xorshift32(seed, n) {
 const res = { node: process.version };
 const file = process.argv[2];
 const reps = Number(process.argv[3] || 3);
+async function main() {
 if (file) {
     const input = fs.readFileSync(file);  // a Buffer: a Uint8Array, as the reference takes
     const n = input.length;
@@ -46,11 +50,11 @@ if (file) {
     const td = [], ti = [];
     for (let r = 0; r < reps; ++r) {
         s = null;
-        gc();
+        await gc();
         let t0 = now();
         s = new RawDeflate(input).compress();
         td.push(now() - t0);
-        gc();
+        await gc();
         t0 = now();
         const inf = new RawInflate(s);
         back = inf.decompress();
@@ -83,3 +87,5 @@ if (!same(o, small)) throw new Error('node bench: 64 KiB round trip mismatch');
 res.c0_64KiB = { stream_bytes: sm.length, deflate_us_per_call: +usd.toFixed(1), inflate_us_per_call: +usi.toFixed(1),
                  deflate_MiBps: +(65536 / 2 ** 20 / (usd / 1e6)).toFixed(1) };
 console.log(JSON.stringify(res));
+}
+main().catch((e) => { console.error(e); process.exit(1); });

@@ -145,6 +145,14 @@ struct DeflateParams {
   int probe;            // near distances 1..probe checked for matches shorter than klen
   int ctype;            // 1: fixed codes only; 2: best of dynamic/fixed/stored
   int opt;              // cost-based parse (optparse_kernel) between match and block kernels
+  // Per-block search depth (0: off): the block's first sub-chunk is searched
+  // with max_chain hops and counts the improvements its walks found at hop
+  // adapt_depth or later (and at hop adapt_depth2 or later); when the first
+  // are at most adapt_thr per 4096 positions, the rest of the block walks
+  // adapt_depth hops, else when the second are at most adapt_thr2,
+  // adapt_depth2 hops (match_kernel)
+  int adapt_depth, adapt_thr;
+  int adapt_depth2, adapt_thr2;
   // batch of independent streams (zt_deflate_batch_dev): stream f occupies
   // whole blocks from a 32 KiB-aligned offset; per block the [start, end) of
   // its stream (relative to halo = 0), or null for one stream of n bytes
@@ -470,6 +478,8 @@ struct MatchShared {
   uint32_t linked;                  // positions below are linked (chain_link -> searching waves)
   uint32_t linked4;                 // positions below have their 4-byte links
   uint32_t work;                    // next super-step of 256 positions to search
+  uint32_t late, late2;             // probe sub-chunk: improvements at hop >= adapt_depth / adapt_depth2
+  int depth;                        // max_chain of the block's later sub-chunks
 };
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS
@@ -748,6 +758,7 @@ struct Walk {
   uint32_t p, q, link, max_len, best_len, best_dist, o, pw, omask, cur, cur2, cur3, cur4;
   uint32_t cl;  // carried match length (kept unless the walk finds one at least as long, nearer)
   int max_hops;  // (hops taken = the pair loop's step count while the walk is active)
+  uint32_t late; // improvements found at hop >= P.adapt_depth (low half) / adapt_depth2 (high half)
   bool active;
 };
 
@@ -766,7 +777,7 @@ __device__ __forceinline__ void ld_run(const MatchShared *s, uint32_t rel, uint3
 // are bytes 0..15 of p
 __device__ __forceinline__ void walk_init(Walk &w, const MatchShared *s, const DeflateParams &P, uint32_t p, uint32_t p1,
                                           uint32_t cur, uint32_t cur2, uint32_t cur3, uint32_t cur4,
-                                          uint32_t carry_len, uint32_t carry_dist, uint32_t link) {
+                                          uint32_t carry_len, uint32_t carry_dist, uint32_t link, int mc) {
   w.p = p;
   w.q = p;
   w.cur = cur;
@@ -780,7 +791,7 @@ __device__ __forceinline__ void walk_init(Walk &w, const MatchShared *s, const D
     w.best_len = carry_len - 1 < w.max_len ? carry_len - 1 : w.max_len;
     w.best_dist = carry_dist;
   }
-  w.max_hops = (int)w.best_len >= P.good ? (P.max_chain >> 2) : P.max_chain;
+  w.max_hops = (int)w.best_len >= P.good ? (mc >> 2) : mc;
   w.active = w.max_len >= (uint32_t)P.klen && (int)w.best_len < P.skip_len;
   w.cl = w.best_len;
 #ifdef ZT_DF_CARRY_TIES
@@ -834,7 +845,8 @@ __device__ __forceinline__ uint32_t eq_len16(uint32_t x0, uint32_t x1, uint32_t 
 
 // a candidate q that passed the one-word filter: its length from byte 0
 // (the filter checked at most 4 bytes) and keep the longest
-__device__ __forceinline__ void walk_extend(Walk &w, const MatchShared *s, const DeflateParams &P, uint32_t q) {
+__device__ __forceinline__ void walk_extend(Walk &w, const MatchShared *s, const DeflateParams &P, uint32_t q,
+                                            uint32_t late) {
 #ifdef ZT_DF_COUNT
   atomicAdd(&g_df_count[2], 1ull);
   // (wave-level executions of the measurement: its first active lane counts)
@@ -866,6 +878,7 @@ __device__ __forceinline__ void walk_extend(Walk &w, const MatchShared *s, const
 #endif
   const bool stop = upd && ((int)len >= P.nice_len || len >= w.max_len);
   const bool newo = upd && !stop && len >= 4;
+  w.late += upd ? late : 0u;
   w.best_len = upd ? len : w.best_len;
   w.best_dist = upd ? w.p - q : w.best_dist;
   w.active = w.active && !stop;
@@ -909,11 +922,13 @@ __device__ __forceinline__ void walk_pair_step(Walk &a, Walk &b, const MatchShar
 #if defined(ZT_DF_X_EXT0)
   // (measurement build: candidates measured at the first hop only -- wrong
   // streams; the time without the later, divergent measurement passes)
-  if (ca && step == 0) walk_extend(a, s, P, qa);
-  if (cb && step == 0) walk_extend(b, s, P, qb);
+  if (ca && step == 0) walk_extend(a, s, P, qa, 0);
+  if (cb && step == 0) walk_extend(b, s, P, qb, 0);
 #else
-  if (ca) walk_extend(a, s, P, qa);
-  if (cb) walk_extend(b, s, P, qb);
+  const uint32_t late = (P.adapt_depth && step >= P.adapt_depth ? 1u : 0u) |
+                        (P.adapt_depth2 && step >= P.adapt_depth2 ? 0x10000u : 0u);
+  if (ca) walk_extend(a, s, P, qa, late);
+  if (cb) walk_extend(b, s, P, qb, late);
 #endif
 }
 
@@ -960,7 +975,7 @@ __device__ __forceinline__ uint32_t walk_finish(const Walk &w, const MatchShared
 // longest match for positions [pb, pb + 4) of the sub-chunk [p0, p1) -> res_out[p - p0];
 // matches end at pml (>= p1)
 __device__ void search_quad(const MatchShared *s, const DeflateParams &P, uint32_t pb, uint32_t p0, uint32_t p1,
-                            uint32_t pml, uint32_t lim4, Key key, uint32_t *res_out) {
+                            uint32_t pml, uint32_t lim4, Key key, uint32_t *res_out, int mc, uint32_t &late) {
   if (pb >= p1) return;
   // bytes [pb - 16, pb + 20) (pb is a multiple of 4; before rel 0 the words
   // are never used: near distances stay <= p)
@@ -979,17 +994,19 @@ __device__ void search_quad(const MatchShared *s, const DeflateParams &P, uint32
   const uint32_t nr0 = near_any<0, 1>(w, win32<16>(w), ~0u), nr1 = near_any<1, 1>(w, win32<17>(w), ~0u);
   const uint32_t nr2 = near_any<2, 1>(w, win32<18>(w), ~0u), nr3 = near_any<3, 1>(w, win32<19>(w), ~0u);
   Walk wa, wb;
-  walk_init(wa, s, P, pb, pml, win32<16>(w), win32<20>(w), win32<24>(w), win32<28>(w), 0, 0, l8.x & 0xFFFFu);
-  walk_init(wb, s, P, pb + 2, pml, win32<18>(w), win32<22>(w), win32<26>(w), win32<30>(w), 0, 0, l8.y & 0xFFFFu);
+  wa.late = wb.late = 0;
+  walk_init(wa, s, P, pb, pml, win32<16>(w), win32<20>(w), win32<24>(w), win32<28>(w), 0, 0, l8.x & 0xFFFFu, mc);
+  walk_init(wb, s, P, pb + 2, pml, win32<18>(w), win32<22>(w), win32<26>(w), win32<30>(w), 0, 0, l8.y & 0xFFFFu, mc);
   for (int step = 0; wa.active || wb.active; ++step) walk_pair_step(wa, wb, s, P, step);
   out[0] = walk_finish<0>(wa, s, P, w, nr0, lim4, l4.x & 0xFFFFu, c0l, c0d);
   out[2] = walk_finish<2>(wb, s, P, w, nr2, lim4, l4.y & 0xFFFFu, c2l, c2d);
 #ifdef ZT_DF_NOCARRY  // experiment: positions 1 and 3 start without the carried match
   c0l = c0d = c2l = c2d = 0;
 #endif
-  walk_init(wa, s, P, pb + 1, pml, win32<17>(w), win32<21>(w), win32<25>(w), win32<29>(w), c0l, c0d, l8.x >> 16);
-  walk_init(wb, s, P, pb + 3, pml, win32<19>(w), win32<23>(w), win32<27>(w), win32<31>(w), c2l, c2d, l8.y >> 16);
+  walk_init(wa, s, P, pb + 1, pml, win32<17>(w), win32<21>(w), win32<25>(w), win32<29>(w), c0l, c0d, l8.x >> 16, mc);
+  walk_init(wb, s, P, pb + 3, pml, win32<19>(w), win32<23>(w), win32<27>(w), win32<31>(w), c2l, c2d, l8.y >> 16, mc);
   for (int step = 0; wa.active || wb.active; ++step) walk_pair_step(wa, wb, s, P, step);
+  late += wa.late + wb.late;
   out[1] = walk_finish<1>(wa, s, P, w, nr1, lim4, l4.x >> 16, cl, cd);
   out[3] = walk_finish<3>(wb, s, P, w, nr3, lim4, l4.y >> 16, cl, cd);
   // the positions' own bytes (res_pack)
@@ -1081,10 +1098,20 @@ __global__ __launch_bounds__(DF_THREADS) void match_kernel(DeflateParams P) {
     if (ih > p1) ih = p1;
     if (rend >= kext && ih > rend - kext) ih = rend - kext;
     const bool link = ih > inserted;
+    // per-block depth: the block's first sub-chunk (the probe) walks max_chain
+    // hops and counts late improvements; its verdict holds for the rest of
+    // the block (a function of the block's own positions: streams do not
+    // depend on how blocks are grouped into workgroups)
+    const bool probe_sub = p0 >= rs && ((p0 - rs) % DF_BLOCK) == 0;
     if (t == 0) {
       s.linked = link ? inserted : ih;
       s.linked4 = link ? inserted : ih;
       s.work = 0;
+      if (p0 > rs && ((p0 - rs) % DF_BLOCK) == DF_SUB)  // (the probe's counts are complete: a barrier since)
+        s.depth = P.adapt_depth && s.late * 4096u <= (uint32_t)P.adapt_thr * DF_SUB     ? P.adapt_depth
+                  : P.adapt_depth2 && s.late2 * 4096u <= (uint32_t)P.adapt_thr2 * DF_SUB ? P.adapt_depth2
+                                                                                          : P.max_chain;
+      if (probe_sub) s.late = s.late2 = 0;
     }
     // the next sub-chunk is fetched while this one is searched
     const uint32_t n0 = p0 + DF_SUB;
@@ -1130,6 +1157,8 @@ __global__ __launch_bounds__(DF_THREADS) void match_kernel(DeflateParams P) {
     inserted = link ? ih : inserted;
     if (p0 >= rs) {
       const uint32_t nss = (p1 - p0 + 255) / 256;
+      const int mc = probe_sub || !P.adapt_depth ? P.max_chain : s.depth;
+      uint32_t late = 0;
       uint32_t *res_out = P.res + (h_lo + p0 - P.halo);  // res[input pos]: rel r <-> input h_lo + r - halo
       for (;;) {
         uint32_t ss = 0;
@@ -1147,13 +1176,19 @@ __global__ __launch_bounds__(DF_THREADS) void match_kernel(DeflateParams P) {
 #ifdef ZT_DF_TIME
         DF_T(w1);
 #endif
-        search_quad(&s, P, p0 + 256 * ss + 4 * (t & 63), p0, p1, pml, ih, key, res_out);
+        search_quad(&s, P, p0 + 256 * ss + 4 * (t & 63), p0, p1, pml, ih, key, res_out, mc, late);
 #ifdef ZT_DF_TIME
         DF_T(w2);
         t_wait += w1 - w0;
         t_srch += w2 - w1;
         n_ss += 1;
 #endif
+      }
+      if (probe_sub && P.adapt_depth) {
+        // (per wave each half stays below 2^16: 256 positions x < 20 hops)
+        for (int o = 32; o; o >>= 1) late += (uint32_t)__shfl_xor((int)late, o, 64);
+        if ((t & 63) == 0 && (late & 0xFFFFu)) atomicAdd(&s.late, late & 0xFFFFu);
+        if ((t & 63) == 0 && (late >> 16)) atomicAdd(&s.late2, late >> 16);
       }
     }
     DF_T(t2);
@@ -2614,9 +2649,37 @@ __global__ __launch_bounds__(256) void stored_blocks(const uint8_t *__restrict__
 // ---- host launcher ---------------------------------------------------------------------------
 struct DeflateLevel {
   int max_chain, nice, lazy, too_far, skip, klen, probe, good, opt;
+  int adapt_depth = 0, adapt_thr = 0, adapt_depth2 = 0, adapt_thr2 = 0;  // per-block depth (DeflateParams)
 };
 
+static DeflateLevel level_params_base(int level);
 static DeflateLevel level_params(int level) {
+  DeflateLevel L = level_params_base(level);
+  // level 6: per-block depth 6 when at most 40 of the probe's 4096 positions
+  // improved at hop 6 or later, else 10 when at most 320 improved at hop 10
+  // or later (the 16-window gate: worst window 1.0190 -> 1.0193, source 0.9875
+  // -> 0.9904; match per GiB: source text 54.2 -> 44.2 ms, structured 16.6 ->
+  // 15.1, the bench corpus 21.0 -> 20.5, wordsalad unchanged;
+  // gpurun_out/r06h, tools/adapt_sweep.py)
+  if (!getenv("ZT_DF_PARAMS") && (level < 1 || level > 9 || level == 6)) {  // (the levels level_params_base maps to 6)
+    L.adapt_depth = 6;
+    L.adapt_thr = 40;
+    L.adapt_depth2 = 10;
+    L.adapt_thr2 = 320;
+  }
+  // tuning hook: ZT_DF_ADAPT="depth,thr[,depth2,thr2]" (per-block depth; depth 0: off)
+  if (const char *e = getenv("ZT_DF_ADAPT")) {
+    int d = 0, t = 0, d2 = 0, t2 = 0;
+    if (sscanf(e, "%d,%d,%d,%d", &d, &t, &d2, &t2) >= 2) {
+      L.adapt_depth = d > 0 && d < L.max_chain ? d : 0;
+      L.adapt_thr = t;
+      L.adapt_depth2 = L.adapt_depth && d2 > d && d2 < L.max_chain ? d2 : 0;
+      L.adapt_thr2 = t2;
+    }
+  }
+  return L;
+}
+static DeflateLevel level_params_base(int level) {
   // tuning hook: ZT_DF_PARAMS="max_chain,nice,lazy,skip,klen,probe[,good[,opt]]" overrides the level
   if (const char *e = getenv("ZT_DF_PARAMS")) {
     DeflateLevel L{64, 128, 1, 4096, 128, 8, 16, 8, 0};
@@ -2769,6 +2832,10 @@ int deflate_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t halo, in
   P.klen = L.klen;
   P.probe = L.probe;
   P.good = L.good;
+  P.adapt_depth = L.adapt_depth;
+  P.adapt_thr = L.adapt_thr;
+  P.adapt_depth2 = L.adapt_depth2;
+  P.adapt_thr2 = L.adapt_thr2;
   P.ctype = ctype;
   P.opt = L.opt && ctype == 2;
   P.span = nullptr;
@@ -2810,9 +2877,15 @@ int deflate_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t halo, in
   ZT_TRY(timing_end(c, s, 1));
   uint64_t total = 0;
   uint32_t nst[2] = {0, 0};  // blocks stored unsearched, encode faults
-  ZT_HIP(hipMemcpyAsync(&total, off + G.nblocks, sizeof total, hipMemcpyDeviceToHost, s));
-  ZT_HIP(hipMemcpyAsync(nst, P.nstore, 8, hipMemcpyDeviceToHost, s));
-  ZT_HIP(hipStreamSynchronize(s));
+  {
+    void *mb;
+    ZT_TRY(mailbox(c, 16, &mb));
+    ZT_HIP(hipMemcpyAsync(mb, off + G.nblocks, sizeof total, hipMemcpyDeviceToHost, s));
+    ZT_HIP(hipMemcpyAsync((uint8_t *)mb + 8, P.nstore, 8, hipMemcpyDeviceToHost, s));
+    ZT_HIP(hipStreamSynchronize(s));
+    memcpy(&total, mb, 8);
+    memcpy(nst, (uint8_t *)mb + 8, 8);
+  }
   if (nst[1]) return set_error(ZT_E_INTERNAL, "deflate: a block's encoded size differs from its plan");
   c->times.blocks_unsearched += nst[0];
   ZT_TRY(timing_collect(c, &c->times.deflate_ms, &c->times.deflate_launches, 0));
@@ -2878,6 +2951,10 @@ int deflate_batch_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t count, const
   P.klen = L.klen;
   P.probe = L.probe;
   P.good = L.good;
+  P.adapt_depth = L.adapt_depth;
+  P.adapt_thr = L.adapt_thr;
+  P.adapt_depth2 = L.adapt_depth2;
+  P.adapt_thr2 = L.adapt_thr2;
   P.ctype = ctype;
   P.opt = L.opt && ctype == 2;
   P.span = d_span;
@@ -2919,9 +2996,16 @@ int deflate_batch_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t count, const
   ZT_TRY(timing_end(c, s, 1));
   std::vector<uint64_t> boff((size_t)G.nblocks + 1);
   uint32_t nst[2] = {0, 0};  // blocks stored unsearched, encode faults
-  ZT_HIP(hipMemcpyAsync(boff.data(), d_off, boff.size() * 8, hipMemcpyDeviceToHost, s));
-  ZT_HIP(hipMemcpyAsync(nst, P.nstore, 8, hipMemcpyDeviceToHost, s));
-  ZT_HIP(hipStreamSynchronize(s));
+  {
+    void *mb;
+    const size_t bb = boff.size() * 8;
+    ZT_TRY(mailbox(c, bb + 8, &mb));
+    ZT_HIP(hipMemcpyAsync(mb, d_off, bb, hipMemcpyDeviceToHost, s));
+    ZT_HIP(hipMemcpyAsync((uint8_t *)mb + bb, P.nstore, 8, hipMemcpyDeviceToHost, s));
+    ZT_HIP(hipStreamSynchronize(s));
+    memcpy(boff.data(), mb, bb);
+    memcpy(nst, (uint8_t *)mb + bb, 8);
+  }
   if (nst[1]) return set_error(ZT_E_INTERNAL, "deflate: a block's encoded size differs from its plan");
   c->times.blocks_unsearched += nst[0];
   ZT_TRY(timing_collect(c, &c->times.deflate_ms, &c->times.deflate_launches, 0));

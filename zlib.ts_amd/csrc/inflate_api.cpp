@@ -113,8 +113,7 @@ static int batch_two_phase(DeviceCtx *c, const uint8_t *d_in, const std::vector<
   BT("tokenize launch");
   ZT_TRY(tokenize_units_dev(tp, s));
   std::vector<TokResult> tr(units);
-  ZT_HIP(hipMemcpyAsync(tr.data(), d_tres, units * sizeof(TokResult), hipMemcpyDeviceToHost, s));
-  ZT_HIP(hipStreamSynchronize(s));
+  ZT_TRY(readback(c, tr.data(), d_tres, units * sizeof(TokResult), s));
   BT("tokenize done");
   // one chain unit and one segment per stream that decoded to BFINAL
   std::vector<ChainUnit> chain;
@@ -265,8 +264,7 @@ static int inflate_dev_batch(DeviceCtx *c, const void *d_in, const std::vector<s
     ZT_TRY(inflate_jobs_dev((const InfJob *)d_jobs, (InfResult *)d_res, (int)todo.size(), c->stream));
     if (pass == 0) c->times.inflate_paths[2] += todo.size();
     std::vector<InfResult> r(todo.size());
-    ZT_HIP(hipMemcpyAsync(r.data(), d_res, todo.size() * sizeof(InfResult), hipMemcpyDeviceToHost, c->stream));
-    ZT_HIP(hipStreamSynchronize(c->stream));
+    ZT_TRY(readback(c, r.data(), d_res, todo.size() * sizeof(InfResult), c->stream));
     std::vector<size_t> again, done;
     // finished outputs are packed on the device side already (out_off);
     // one D2H of the span up to the last finished byte into pinned staging
@@ -429,41 +427,61 @@ static int inflate_raw_pipelined(DeviceCtx *c, const uint8_t *in, size_t n, size
   if (np < 2) return 1;
   void *d_in;
   ZT_TRY(scratch(c, 0, m + 64 * np + 256, &d_in));
-  // Results go to a ring of kRing device buffers (scratch slots 22..24):
-  // piece i decodes into slot 22 + i % kRing once piece i - kRing's bytes have
-  // left the device.  A slot is sized 4x its piece's input, or from piece 0's
-  // output ratio when that is higher, and grown to what a piece reports it
-  // needs (one more decode of that piece); the host output starts at piece 0's
-  // ratio x the stream and grows the same way (pipeline_h2d_d2h), so a stream
-  // of any ratio stays pipelined.
+  // Results go to one device buffer at consecutive offsets (scratch slot 22,
+  // 4x the input, as the host output used to be), each piece's capacity 4x
+  // its input or what is left, and a piece that reports needing more is
+  // decoded again with that.  Past the buffer's end (streams compressed
+  // better than 4:1) the pieces go to a ring of 3 overflow buffers (slots
+  // 23-25), piece i's once piece i - 3's bytes have left the device
+  // (PipeOut::drain).  The host output starts at piece 0's ratio x the
+  // stream and grows the same way (pipeline_h2d_d2h), so a stream of any
+  // ratio stays pipelined.
   constexpr size_t kRing = 3;
   auto d_piece = [&](size_t i) { return (uint8_t *)d_in + (cut[i] - index) + 64 * i; };
-  double ratio0 = 0;  // output bytes per input byte of piece 0
+  const size_t cap = std::max<size_t>(4 * m, 64u << 20);
+  void *d_big;
+  ZT_TRY(scratch(c, 22, cap, &d_big));
+  size_t off = 0;      // bytes of the big buffer used
+  size_t ring0 = np;   // first piece in the overflow ring
+  double ratio0 = 0;   // output bytes per input byte of piece 0
   size_t eip_last = 0;
   PipeOut po;
-  po.ring = kRing;
   po.cap_fn = [&] { return (size_t)(ratio0 * 1.25 * (double)m) + (16u << 20); };
   const int rc = pipeline_h2d_d2h(
       c, np, [&](size_t i) { return PipePiece{in + cut[i], d_piece(i), cut[i + 1] - cut[i]}; },
       [&](size_t i, const void **d_res, size_t *n_res) -> int {
         const size_t len = cut[i + 1] - cut[i];
         const bool last = i + 1 == np;
-        if (!last) ZT_HIP(hipMemcpyAsync(d_piece(i) + len, kFinal, sizeof kFinal, hipMemcpyHostToDevice, c->stream));
+        if (!last) {  // kFinal by fills: no host bytes to stage behind the pipeline's uploads
+          ZT_HIP(hipMemsetAsync(d_piece(i) + len, kFinal[0], 1, c->stream));
+          ZT_HIP(hipMemsetAsync(d_piece(i) + len + 1, 0, 2, c->stream));
+          ZT_HIP(hipMemsetAsync(d_piece(i) + len + 3, 0xFF, 2, c->stream));
+        }
         const size_t pn = last ? len : len + sizeof kFinal;
-        const int slot = 22 + (int)(i % kRing);
         size_t want = 4 * pn + (1u << 20);
         if (i > 0) want = std::max(want, (size_t)(ratio0 * 1.25 * (double)pn) + (1u << 20));
         for (int attempt = 0; attempt < 2; ++attempt) {
-          void *p;
-          ZT_TRY(scratch(c, slot, want, &p));
-          uint8_t *d_o = static_cast<uint8_t *>(p);
-          const size_t ocap = c->buf_size[slot];
+          uint8_t *d_o;
+          size_t ocap;
+          // (first try: whatever room is left, at least 1 MiB; again: all it needs)
+          if (i < ring0 && (attempt == 0 ? off + (1u << 20) <= cap : off + want <= cap)) {
+            d_o = static_cast<uint8_t *>(d_big) + off;
+            ocap = std::min(want, cap - off);
+          } else {  // the overflow ring
+            if (ring0 == np) ring0 = i;
+            const size_t r = (i - ring0) % kRing;
+            if (i - ring0 >= kRing) ZT_TRY(po.drain(i - kRing));
+            void *p;
+            ZT_TRY(scratch(c, 23 + (int)r, want, &p));
+            d_o = static_cast<uint8_t *>(p);
+            ocap = want;  // (the capacity asked: the device chain sizes its descriptors from it)
+          }
           size_t ol = 0, eip = 0;
           // a non-final piece must have a block boundary right before its
           // appended final block (the cut) -- and must end on that block
           int seg = inflate_segments_dev(c, d_piece(i), pn, 0, &d_o, ocap, &ol, &eip, c->stream, last ? ~0ull : len);
-          if (seg < 0 && ol > ocap && attempt == 0) {  // more output than the slot: grow it, decode again
-            want = ol + (1u << 20);
+          if (seg < 0 && ol > ocap && attempt == 0) {  // more output than its room: again with what it needs
+            want = ol;
             continue;
           }
           // (no sync points in the last piece: the speculative general decoder)
@@ -471,6 +489,7 @@ static int inflate_raw_pipelined(DeviceCtx *c, const uint8_t *in, size_t n, size
           if (seg != 0) return seg < 0 ? seg : set_error(ZT_E_INTERNAL, "pipelined inflate: piece not decoded");
           if (!last && eip != pn) return set_error(ZT_E_INTERNAL, "pipelined inflate: a cut is not a block boundary");
           if (i == 0) ratio0 = (double)ol / (double)pn;
+          if (i < ring0) off += (ol + 255) & ~(size_t)255;
           eip_last = eip;
           *d_res = d_o;
           *n_res = ol;
@@ -589,8 +608,7 @@ static int resume_impl(const uint8_t *in, size_t n, uint64_t bit_pos, const uint
     InfResult r;
     ZT_HIP(hipMemcpyAsync(d_jobs, &j, sizeof j, hipMemcpyHostToDevice, c->stream));
     ZT_TRY(inflate_jobs_dev((const InfJob *)d_jobs, d_res, 1, c->stream));
-    ZT_HIP(hipMemcpyAsync(&r, d_res, sizeof r, hipMemcpyDeviceToHost, c->stream));
-    ZT_HIP(hipStreamSynchronize(c->stream));
+    ZT_TRY(readback(c, &r, d_res, sizeof r, c->stream));
     // running out of input (the reader's end-of-input statuses, or any error
     // within the last 64 bits, where a peek may have seen the zeros past the
     // end) means "more input needed"; an error before that is the stream's own

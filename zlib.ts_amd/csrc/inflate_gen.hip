@@ -832,21 +832,16 @@ int inflate_general_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t inde
                                                            d_cnt + 1);
   ZT_HIP(hipGetLastError());
   uint32_t cnts[2];
-  ZT_HIP(hipMemcpyAsync(cnts, d_cnt, 8, hipMemcpyDeviceToHost, s));
-  ZT_HIP(hipStreamSynchronize(s));
+  ZT_TRY(readback(c, cnts, d_cnt, 8, s));
   const uint32_t nb = std::min(cnts[0], kMaxCandB);
   if (nb) {
     check_headers<<<(nb + 255) / 256, 256, 0, s>>>(d_in, n, d_listb, d_cnt, d_list, d_cnt + 1);
     ZT_HIP(hipGetLastError());
   }
-  ZT_HIP(hipMemcpyAsync(cnts, d_cnt, 8, hipMemcpyDeviceToHost, s));
-  ZT_HIP(hipStreamSynchronize(s));
+  ZT_TRY(readback(c, cnts, d_cnt, 8, s));
   const uint32_t nc = std::min(cnts[1], kMaxCand);
   std::vector<uint64_t> cand(nc);
-  if (nc) {
-    ZT_HIP(hipMemcpyAsync(cand.data(), d_list, (size_t)nc * 8, hipMemcpyDeviceToHost, s));
-    ZT_HIP(hipStreamSynchronize(s));
-  }
+  if (nc) ZT_TRY(readback(c, cand.data(), d_list, (size_t)nc * 8, s));
   radix_sort64(cand, (bitn << 17) | 0x1FFFF);  // entry: bit position << 17 | stored LEN << 1 | stored
   // stored candidates are hints with false positives (LEN = ~NLEN inside any
   // data): keep one only when a candidate starts where its payload ends (the
@@ -998,9 +993,16 @@ int inflate_general_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t inde
       gen_link_kernel<<<(uint32_t)ltodo.size(), 64, 0, s>>>(d_jobs, d_res, gp.bm, gp.tokens, d_lwhich, d_link);
       ZT_HIP(hipGetLastError());
     }
-    ZT_HIP(hipMemcpyAsync(res.data(), d_res, units * sizeof(GenResult), hipMemcpyDeviceToHost, s));
-    ZT_HIP(hipMemcpyAsync(link.data(), d_link, units * sizeof(GenLink), hipMemcpyDeviceToHost, s));
-    ZT_HIP(hipStreamSynchronize(s));
+    {
+      void *mb;
+      const size_t rb = units * sizeof(GenResult), lb = units * sizeof(GenLink);
+      ZT_TRY(mailbox(c, rb + lb, &mb));
+      ZT_HIP(hipMemcpyAsync(mb, d_res, rb, hipMemcpyDeviceToHost, s));
+      ZT_HIP(hipMemcpyAsync((uint8_t *)mb + rb, d_link, lb, hipMemcpyDeviceToHost, s));
+      ZT_HIP(hipStreamSynchronize(s));
+      memcpy(res.data(), mb, rb);
+      memcpy(link.data(), (uint8_t *)mb + rb, lb);
+    }
     // walk the chain (past broken units too: independent failures are all
     // redone in the same pass)
     std::vector<uint32_t> bad;
@@ -1227,9 +1229,15 @@ int inflate_general_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t inde
   ZT_HIP(hipGetLastError());
   ZT_TRY(timing_end(c, s, 2));
   std::vector<int32_t> ust(chain.size()), sst(segs.size());
-  ZT_HIP(hipMemcpyAsync(ust.data(), d_ust, chain.size() * 4, hipMemcpyDeviceToHost, s));
-  ZT_HIP(hipMemcpyAsync(sst.data(), d_st, segs.size() * 4, hipMemcpyDeviceToHost, s));
-  ZT_HIP(hipStreamSynchronize(s));
+  {
+    void *mb;
+    ZT_TRY(mailbox(c, (chain.size() + segs.size()) * 4, &mb));
+    ZT_HIP(hipMemcpyAsync(mb, d_ust, chain.size() * 4, hipMemcpyDeviceToHost, s));
+    ZT_HIP(hipMemcpyAsync((uint8_t *)mb + chain.size() * 4, d_st, segs.size() * 4, hipMemcpyDeviceToHost, s));
+    ZT_HIP(hipStreamSynchronize(s));
+    memcpy(ust.data(), mb, chain.size() * 4);
+    memcpy(sst.data(), (uint8_t *)mb + chain.size() * 4, segs.size() * 4);
+  }
   ZT_TRY(timing_collect(c, &c->times.inflate_ms, &c->times.inflate_launches, 2));
   for (size_t i = 0; i < chain.size(); ++i)
     if (ust[i] != ZT_OK) GFALLBACK("chain unit %zu: status %d\n", i, ust[i]);

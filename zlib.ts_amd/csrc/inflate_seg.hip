@@ -520,8 +520,7 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   find_syncs<<<grid, 256, 0, s>>>(d_in, index, n, d_list, d_count);
   ZT_HIP(hipGetLastError());
   uint32_t cnt = 0;
-  ZT_HIP(hipMemcpyAsync(&cnt, d_count, 4, hipMemcpyDeviceToHost, s));
-  ZT_HIP(hipStreamSynchronize(s));
+  ZT_TRY(readback(c, &cnt, d_count, 4, s));
   IT("sync points counted");
   if (cnt == 0 || cnt > kMaxSync) FALLBACK("%u sync points\n", cnt);
   // 2. the candidates sorted, deduplicated and turned into units on the
@@ -574,10 +573,17 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   unit_slots<<<g, 256, 0, s>>>(d_off, d_slot, d_pos + cnt, d_jobs, d_ttot);
   ZT_HIP(hipGetLastError());
   uint64_t tot_h[3] = {0, 0, 0};
-  ZT_HIP(hipMemcpyAsync(&tot_h[0], d_ttot, 8, hipMemcpyDeviceToHost, s));
-  ZT_HIP(hipMemcpyAsync(&tot_h[1], d_pos + cnt, 4, hipMemcpyDeviceToHost, s));
-  ZT_HIP(hipMemcpyAsync(&tot_h[2], d_ttot + 2, 4, hipMemcpyDeviceToHost, s));
-  ZT_HIP(hipStreamSynchronize(s));
+  {
+    void *mb;
+    ZT_TRY(mailbox(c, 24, &mb));
+    uint64_t *m64 = static_cast<uint64_t *>(mb);
+    m64[1] = m64[2] = 0;
+    ZT_HIP(hipMemcpyAsync(&m64[0], d_ttot, 8, hipMemcpyDeviceToHost, s));
+    ZT_HIP(hipMemcpyAsync(&m64[1], d_pos + cnt, 4, hipMemcpyDeviceToHost, s));
+    ZT_HIP(hipMemcpyAsync(&m64[2], d_ttot + 2, 4, hipMemcpyDeviceToHost, s));
+    ZT_HIP(hipStreamSynchronize(s));
+    for (int k = 0; k < 3; ++k) tot_h[k] = m64[k];
+  }
   IT("units counted");
   const uint32_t nsync = (uint32_t)tot_h[1];
   const size_t units = (size_t)nsync + 1;
@@ -800,8 +806,7 @@ host_walk:
   }
   if (boundary != ~0ull) {
     std::vector<TokJob> hj(units);
-    ZT_HIP(hipMemcpyAsync(hj.data(), d_jobs, units * sizeof(TokJob), hipMemcpyDeviceToHost, s));
-    ZT_HIP(hipStreamSynchronize(s));
+    ZT_TRY(readback(c, hj.data(), d_jobs, units * sizeof(TokJob), s));
     bool at = false;
     for (size_t k : chained) at = at || hj[k].start == boundary;
     if (!at) FALLBACK("no unit of the chain starts at the boundary %llu\n", (unsigned long long)boundary);

@@ -5,6 +5,7 @@
 #include <sys/mman.h>
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
 #include <functional>
 #include <map>
@@ -342,6 +343,18 @@ int pinned(DeviceCtx *c, size_t bytes, void **ptr, int slot) {
   return ZT_OK;
 }
 
+int mailbox(DeviceCtx *c, size_t n, void **p) { return pinned(c, n < 4096 ? 4096 : n, p, 8); }
+
+int readback(DeviceCtx *c, void *h_dst, const void *d_src, size_t n, hipStream_t s) {
+  if (!n) return ZT_OK;
+  void *mb;
+  ZT_TRY(mailbox(c, n, &mb));
+  ZT_HIP(hipMemcpyAsync(mb, d_src, n, hipMemcpyDeviceToHost, s));
+  ZT_HIP(hipStreamSynchronize(s));
+  memcpy(h_dst, mb, n);
+  return ZT_OK;
+}
+
 // Large host buffers move through two pinned 32 MiB chunks: the host copy of
 // chunk k + 1 (a few threads) overlaps the DMA of chunk k -- pageable
 // hipMemcpy stages through the runtime's own small buffers at a fraction of
@@ -426,8 +439,20 @@ int download(DeviceCtx *c, void *h_dst, const void *d_src, size_t n, hipStream_t
 // caller's thread, where zt_last_error_message() reads it).  Every stream the
 // pipeline used is drained before it returns, on error paths too: the caller
 // may free the output (or the input) as soon as it has the status.
+// ZT_PIPE_TIMING=1: per-piece stage timestamps on stderr (measurement only)
+static double pt_now() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+static bool pt_on() {
+  static const bool on = getenv("ZT_PIPE_TIMING") != nullptr;
+  return on;
+}
+#define PT(...) \
+  if (pt_on()) fprintf(stderr, "[pipe %9.3f] " __VA_ARGS__)
+
 int pipeline_h2d_d2h(DeviceCtx *c, size_t np, const std::function<PipePiece(size_t)> &input,
                      const std::function<int(size_t, const void **d_res, size_t *n_res)> &compute, PipeOut &out) {
+  const double t_start = pt_now();
   if (!c->up) ZT_HIP(hipStreamCreateWithFlags(&c->up, hipStreamNonBlocking));
   if (!c->dn) ZT_HIP(hipStreamCreateWithFlags(&c->dn, hipStreamNonBlocking));
   uint8_t *stage[4];
@@ -446,8 +471,7 @@ int pipeline_h2d_d2h(DeviceCtx *c, size_t np, const std::function<PipePiece(size
     }
   } ev_free{landed}, ev_free2{drained};
   for (auto &e : landed) ZT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  if (out.ring)
-    for (auto &e : drained) ZT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  for (auto &e : drained) ZT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
 
   std::mutex mu;
   std::condition_variable cv;
@@ -488,6 +512,7 @@ int pipeline_h2d_d2h(DeviceCtx *c, size_t np, const std::function<PipePiece(size
         ZT_HIP(hipEventRecord(c->xfer_ev[k & 1], c->up));
       }
       ZT_HIP(hipEventRecord(landed[i], c->up));
+      PT("up %zu issued (%zu B, %s)\n", pt_now() - t_start, i, pc.n, host_direct(pc.h_src, pc.n) ? "direct" : "staged");
       std::lock_guard<std::mutex> lk(mu);
       uploaded = i + 1;
       cv.notify_all();
@@ -513,7 +538,9 @@ int pipeline_h2d_d2h(DeviceCtx *c, size_t np, const std::function<PipePiece(size
         base = host_out(cap, true);
         if (!base) return set_error(ZT_E_NOMEM, "host allocation failed");
       }
+      PT("dn %zu start (%zu B)\n", pt_now() - t_start, i, n);
       if (total + n > cap) {  // a larger buffer: the bytes so far move over
+        PT("dn %zu grows the output %zu -> ...\n", pt_now() - t_start, i, cap);
         const size_t ncap = std::max(2 * cap, total + n + (total + n) / 4);
         uint8_t *nb = host_out(ncap, true);
         if (!nb) return set_error(ZT_E_NOMEM, "host allocation failed");
@@ -525,7 +552,9 @@ int pipeline_h2d_d2h(DeviceCtx *c, size_t np, const std::function<PipePiece(size
       }
       if (host_direct(base + total, n)) {
         if (n) ZT_HIP(hipMemcpyAsync(base + total, res[i], n, hipMemcpyDeviceToHost, c->dn));
+        PT("dn %zu direct\n", pt_now() - t_start, i);
       } else {
+        PT("dn %zu staged\n", pt_now() - t_start, i);
         // chunks of this piece: issue k + 1 before copying k out of its staging buffer
         const size_t nch = (n + kXferChunk - 1) / kXferChunk;
         auto issue = [&](size_t j) -> int {
@@ -545,11 +574,20 @@ int pipeline_h2d_d2h(DeviceCtx *c, size_t np, const std::function<PipePiece(size
         k += nch;
       }
       total += n;
-      if (out.ring) ZT_HIP(hipEventRecord(drained[i], c->dn));
+      ZT_HIP(hipEventRecord(drained[i], c->dn));
       std::lock_guard<std::mutex> lk(mu);
       downloaded = i + 1;
       cv.notify_all();
     }
+    return ZT_OK;
+  };
+  out.drain = [&](size_t j) -> int {
+    {
+      std::unique_lock<std::mutex> lk(mu);
+      cv.wait(lk, [&] { return downloaded > j || err; });
+      if (err) return set_error(ZT_E_INTERNAL, "pipeline stopped");
+    }
+    ZT_HIP(hipStreamWaitEvent(c->stream, drained[j], 0));
     return ZT_OK;
   };
   std::thread tu([&] {
@@ -558,21 +596,20 @@ int pipeline_h2d_d2h(DeviceCtx *c, size_t np, const std::function<PipePiece(size
   std::thread td([&] {
     if (int rc = dn_stage()) fail(rc);
   });
-  // stage 2 on the caller's thread: compute(i) after piece i has landed (and,
-  // with a ring, after piece i - ring's result has left the device)
+  // stage 2 on the caller's thread: compute(i) after piece i has landed
   for (size_t i = 0; i < np; ++i) {
     {
       std::unique_lock<std::mutex> lk(mu);
-      cv.wait(lk, [&] { return (uploaded > i && (!out.ring || i < out.ring || downloaded > i - out.ring)) || err; });
+      cv.wait(lk, [&] { return uploaded > i || err; });
       if (err) break;
     }
     int rc = hipStreamWaitEvent(c->stream, landed[i], 0) == hipSuccess ? ZT_OK
                                                                        : set_error(ZT_E_HIP, "hipStreamWaitEvent");
-    if (!rc && out.ring && i >= out.ring && hipStreamWaitEvent(c->stream, drained[i - out.ring], 0) != hipSuccess)
-      rc = set_error(ZT_E_HIP, "hipStreamWaitEvent");
     const void *d = nullptr;
     size_t m = 0;
+    PT("compute %zu start\n", pt_now() - t_start, i);
     if (!rc) rc = compute(i, &d, &m);
+    PT("compute %zu done (%zu B)\n", pt_now() - t_start, i, m);
     if (rc) {
       fail(rc);
       break;
@@ -585,10 +622,13 @@ int pipeline_h2d_d2h(DeviceCtx *c, size_t np, const std::function<PipePiece(size
   }
   tu.join();
   td.join();
+  PT("joined\n", pt_now() - t_start);
   // nothing may still be copying into the output or out of the input when
   // the caller gets it back (error paths: zt_free / reuse right after)
   const hipError_t e1 = hipStreamSynchronize(c->up), e2 = hipStreamSynchronize(c->dn),
                    e3 = hipStreamSynchronize(c->stream);
+  PT("drained\n", pt_now() - t_start);
+  out.drain = nullptr;
   out.base = base;
   out.cap = cap;
   out.total = total;
@@ -757,7 +797,7 @@ int zt_release_scratch(void) {
     c->d_buf[k] = nullptr;
     c->buf_size[k] = 0;
   }
-  for (int k = 0; k < 8; ++k) {
+  for (int k = 0; k < 10; ++k) {
     if (c->h_pinned[k]) ZT_HIP(hipHostFree(c->h_pinned[k]));
     c->h_pinned[k] = nullptr;
     c->pinned_size[k] = 0;

@@ -55,21 +55,22 @@ struct DeviceCtx {
   static constexpr int kSlots = 26;
   void *d_buf[kSlots] = {};  // slot 8: checksum segment partials; 10-17: general inflate (inflate_gen.hip);
                              // 20: segment inflate's sync-point sort (inflate_seg.hip); 21: stored runs;
-                             // 22-24: pipelined host inflate's output ring (inflate_api.cpp)
+                             // 22: pipelined host inflate's output, 23-25: its overflow ring (inflate_api.cpp)
   size_t buf_size[kSlots] = {};
   // second stream: checksums run beside the deflate pipeline in the containers
   hipStream_t aux = nullptr;
   hipEvent_t aux_ev = nullptr;
-  void *h_pinned[8] = {};  // pinned host staging: 0 batch data, 1 inflate metadata, 2-3 upload/download chunks,
-                           // 4-5 download chunks of the three-stage pipeline (pipeline_h2d_d2h),
-                           // 6-7 second input group / output group of a grouped batch (batch_api.cpp)
+  void *h_pinned[10] = {};  // pinned host staging: 0 batch data, 1 inflate metadata, 2-3 upload/download chunks,
+                            // 4-5 download chunks of the three-stage pipeline (pipeline_h2d_d2h),
+                            // 6-7 second input group / output group of a grouped batch (batch_api.cpp),
+                            // 8 the readback mailbox (mailbox())
   hipEvent_t xfer_ev[4] = {};  // chunk buffer 2 + k's copy has finished
   hipStream_t up = nullptr, dn = nullptr;  // pipeline_h2d_d2h: H2D and D2H copy streams
   // zt_timing_enable: HIP-event kernel timing
   bool timing = false;
   hipEvent_t ev[8] = {};  // [2k, 2k+1]: interval k (0 match, 1 deflate pipeline, 2 inflate)
   zt_kernel_times times = {};
-  size_t pinned_size[8] = {};
+  size_t pinned_size[10] = {};
 };
 
 // Records the begin / end event of interval k (0 or 1) when timing is on.
@@ -84,6 +85,16 @@ int get_ctx(DeviceCtx **out);
 int scratch(DeviceCtx *c, int slot, size_t bytes, void **ptr);
 // Grow-only pinned host staging buffer `slot` (0 or 1) of at least `bytes`.
 int pinned(DeviceCtx *c, size_t bytes, void **ptr, int slot = 0);
+// Small device -> host readbacks (counts, per-unit results) go through
+// pinned memory: into a pageable destination hipMemcpyAsync stages through
+// the runtime and waits behind the large copies other streams have queued --
+// the host pipelines' uploads and downloads -- 1-4 ms per readback there.
+// mailbox(c, n): a pinned region of >= n bytes (pinned slot 8), valid until
+// the next mailbox call (one user at a time: the context's caller thread).
+int mailbox(DeviceCtx *c, size_t n, void **p);
+// readback(c, dst, src, n, s): n bytes from the device to dst through the
+// mailbox, synchronous (s is synchronized)
+int readback(DeviceCtx *c, void *h_dst, const void *d_src, size_t n, hipStream_t s);
 // Host output buffer the caller frees with zt_free (large ones on huge pages;
 // pool = true: from the bounded host output pool, zt_api.cpp); host_release
 // is zt_free's second half (back to the pool, or free).  host_direct: [p,
@@ -386,10 +397,11 @@ struct PipeOut {
   uint8_t *base = nullptr;
   size_t cap = 0;
   std::function<size_t()> cap_fn;
-  // > 0: compute(i) starts only after piece i - ring's result has left the
-  // device (device result buffers reused round robin)
-  size_t ring = 0;
   size_t total = 0;  // out: bytes written
+  // set by the pipeline for compute(i): drain(j), j < i, makes the compute
+  // stream wait until piece j's result has left the device (before compute
+  // reuses its device buffer); waits on the host until that copy is issued
+  std::function<int(size_t)> drain;
 };
 int pipeline_h2d_d2h(DeviceCtx *c, size_t np, const std::function<PipePiece(size_t)> &input,
                      const std::function<int(size_t, const void **d_res, size_t *n_res)> &compute, PipeOut &out);
