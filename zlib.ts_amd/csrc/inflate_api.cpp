@@ -446,16 +446,22 @@ static int inflate_raw_pipelined(DeviceCtx *c, const uint8_t *in, size_t n, size
   double ratio0 = 0;   // output bytes per input byte of piece 0
   size_t eip_last = 0;
   PipeOut po;
+  static const bool eager = getenv("ZT_INF_EAGER") != nullptr;  // (A/B hook: the host output allocated up front, 4x)
+  if (eager) {
+    po.base = host_out(cap, true);
+    po.cap = cap;
+    if (!po.base) return set_error(ZT_E_NOMEM, "host allocation failed");
+  }
   po.cap_fn = [&] { return (size_t)(ratio0 * 1.25 * (double)m) + (16u << 20); };
   const int rc = pipeline_h2d_d2h(
       c, np, [&](size_t i) { return PipePiece{in + cut[i], d_piece(i), cut[i + 1] - cut[i]}; },
       [&](size_t i, const void **d_res, size_t *n_res) -> int {
         const size_t len = cut[i + 1] - cut[i];
         const bool last = i + 1 == np;
-        if (!last) {  // kFinal by fills: no host bytes to stage behind the pipeline's uploads
-          ZT_HIP(hipMemsetAsync(d_piece(i) + len, kFinal[0], 1, c->stream));
-          ZT_HIP(hipMemsetAsync(d_piece(i) + len + 1, 0, 2, c->stream));
-          ZT_HIP(hipMemsetAsync(d_piece(i) + len + 3, 0xFF, 2, c->stream));
+        if (!last) {  // (by a kernel: no copy-engine command queued behind the pipeline's transfers)
+          uint64_t fin = 0;
+          for (int k = 0; k < (int)sizeof kFinal; ++k) fin |= (uint64_t)kFinal[k] << (8 * k);
+          ZT_TRY(q_bytes(d_piece(i) + len, fin, (uint32_t)sizeof kFinal, c->stream));
         }
         const size_t pn = last ? len : len + sizeof kFinal;
         size_t want = 4 * pn + (1u << 20);

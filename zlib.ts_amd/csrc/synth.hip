@@ -2,6 +2,8 @@
 // Piece i (64 KiB) of a buffer is generator `kind` seeded with seed + i, so a
 // piece equals tools/gen_golden.mjs / oracle zo_gen(kind, seed + i, 65536).
 // kind 3 ("mixed") cycles wordsalad / xorshift32 / structured per 4 MiB window.
+#include <algorithm>
+
 #include "zt_internal.h"
 
 namespace zt {
@@ -82,7 +84,41 @@ __global__ __launch_bounds__(64) void synth_kernel(int kind, uint32_t seed, uint
   o.finish(out + lo);
 }
 
+// small copies by a kernel (q_copy): dwords when both ends are 4-byte aligned
+__global__ __launch_bounds__(256) void q_copy_kernel(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src,
+                                                     uint64_t n) {
+  const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x, stride = (uint64_t)gridDim.x * 256;
+  if (((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 3) == 0) {
+    const uint64_t nw = n >> 2;
+    for (uint64_t i = t; i < nw; i += stride)
+      reinterpret_cast<uint32_t *>(dst)[i] = reinterpret_cast<const uint32_t *>(src)[i];
+    for (uint64_t i = (nw << 2) + t; i < n; i += stride) dst[i] = src[i];
+  } else {
+    for (uint64_t i = t; i < n; i += stride) dst[i] = src[i];
+  }
+}
+
+__global__ void q_bytes_kernel(uint8_t *dst, uint64_t v, uint32_t n) {
+  if (threadIdx.x < n) dst[threadIdx.x] = (uint8_t)(v >> (8 * threadIdx.x));
+}
+
 }  // namespace
+
+int q_bytes(void *dst, uint64_t v, uint32_t n, hipStream_t s) {
+  if (!n) return ZT_OK;
+  q_bytes_kernel<<<1, 64, 0, s>>>(static_cast<uint8_t *>(dst), v, n);
+  ZT_HIP(hipGetLastError());
+  return ZT_OK;
+}
+
+int q_copy(void *dst, const void *src, size_t n, hipStream_t s) {
+  if (!n) return ZT_OK;
+  const uint64_t blocks = std::min<uint64_t>(1024, (n / 4 + 255) / 256 + 1);
+  q_copy_kernel<<<(unsigned)blocks, 256, 0, s>>>(static_cast<uint8_t *>(dst), static_cast<const uint8_t *>(src), n);
+  ZT_HIP(hipGetLastError());
+  return ZT_OK;
+}
+
 }  // namespace zt
 
 using namespace zt;

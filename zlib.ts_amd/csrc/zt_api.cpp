@@ -332,7 +332,8 @@ int pinned(DeviceCtx *c, size_t bytes, void **ptr, int slot) {
       c->pinned_size[slot] = 0;
     }
     size_t sz = bytes + bytes / 4;
-    if (const hipError_t e = hipHostMalloc(&c->h_pinned[slot], sz, hipHostMallocDefault)) {
+    // (slot 1, the inflate metadata, is written and read by q_copy kernels: coherent)
+    if (const hipError_t e = hipHostMalloc(&c->h_pinned[slot], sz, slot == 1 ? hipHostMallocCoherent : hipHostMallocDefault)) {
       c->h_pinned[slot] = nullptr;
       (void)hipGetLastError();
       return hip_fail(e, "hipHostMalloc (staging)");
@@ -343,13 +344,34 @@ int pinned(DeviceCtx *c, size_t bytes, void **ptr, int slot) {
   return ZT_OK;
 }
 
-int mailbox(DeviceCtx *c, size_t n, void **p) { return pinned(c, n < 4096 ? 4096 : n, p, 8); }
+int mailbox(DeviceCtx *c, size_t n, void **p) {
+  constexpr int kSlot = 8;
+  if (n < 4096) n = 4096;
+  if (c->pinned_size[kSlot] < n) {
+    if (c->h_pinned[kSlot]) {
+      ZT_HIP(hipDeviceSynchronize());
+      ZT_HIP(hipHostFree(c->h_pinned[kSlot]));
+      c->h_pinned[kSlot] = nullptr;
+      c->pinned_size[kSlot] = 0;
+    }
+    const size_t sz = n + n / 4;
+    // coherent: the kernels' stores are visible to the host once the stream is synchronized
+    if (const hipError_t e = hipHostMalloc(&c->h_pinned[kSlot], sz, hipHostMallocCoherent)) {
+      c->h_pinned[kSlot] = nullptr;
+      (void)hipGetLastError();
+      return hip_fail(e, "hipHostMalloc (mailbox)");
+    }
+    c->pinned_size[kSlot] = sz;
+  }
+  *p = c->h_pinned[kSlot];
+  return ZT_OK;
+}
 
 int readback(DeviceCtx *c, void *h_dst, const void *d_src, size_t n, hipStream_t s) {
   if (!n) return ZT_OK;
   void *mb;
   ZT_TRY(mailbox(c, n, &mb));
-  ZT_HIP(hipMemcpyAsync(mb, d_src, n, hipMemcpyDeviceToHost, s));
+  ZT_TRY(q_copy(mb, d_src, n, s));
   ZT_HIP(hipStreamSynchronize(s));
   memcpy(h_dst, mb, n);
   return ZT_OK;

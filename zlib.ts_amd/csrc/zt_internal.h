@@ -52,10 +52,11 @@ struct DeviceCtx {
   uint32_t *d_crc_shift = nullptr;  // checksum.hip merge constants (crc_shift_tables)
   CkAcc *d_ck_acc = nullptr;        // checksum merge accumulators (zeroed once, left zeroed by every call)
   // scratch
-  static constexpr int kSlots = 26;
+  static constexpr int kSlots = 27;
   void *d_buf[kSlots] = {};  // slot 8: checksum segment partials; 10-17: general inflate (inflate_gen.hip);
                              // 20: segment inflate's sync-point sort (inflate_seg.hip); 21: stored runs;
-                             // 22: pipelined host inflate's output, 23-25: its overflow ring (inflate_api.cpp)
+                             // 22: pipelined host inflate's output, 23-25: its overflow ring (inflate_api.cpp);
+                             // 26: general inflate's window pointer-jumping buffers
   size_t buf_size[kSlots] = {};
   // second stream: checksums run beside the deflate pipeline in the containers
   hipStream_t aux = nullptr;
@@ -85,15 +86,21 @@ int get_ctx(DeviceCtx **out);
 int scratch(DeviceCtx *c, int slot, size_t bytes, void **ptr);
 // Grow-only pinned host staging buffer `slot` (0 or 1) of at least `bytes`.
 int pinned(DeviceCtx *c, size_t bytes, void **ptr, int slot = 0);
-// Small device -> host readbacks (counts, per-unit results) go through
-// pinned memory: into a pageable destination hipMemcpyAsync stages through
-// the runtime and waits behind the large copies other streams have queued --
-// the host pipelines' uploads and downloads -- 1-4 ms per readback there.
-// mailbox(c, n): a pinned region of >= n bytes (pinned slot 8), valid until
-// the next mailbox call (one user at a time: the context's caller thread).
+// Small transfers between the host and the device (counts, per-unit
+// results, chain tables) are made by a kernel on the calling stream over
+// pinned host memory the GPU addresses directly, not by the copy engines:
+// hipMemcpyAsync of a few bytes queues behind the large copies the host
+// pipelines keep on the engines (their uploads and downloads, 32-180 MB
+// each) and waited 1-4 ms per transfer there, and a pageable destination
+// adds a staging copy.  q_copy(dst, src, n, s): the kernel copy (either end
+// device or pinned host memory).  mailbox(c, n): a pinned, coherent region of
+// >= n bytes (pinned slot 8), valid until the next mailbox call (one user at
+// a time: the context's caller thread).  readback(c, dst, src, n, s): n bytes
+// from the device to any host dst through the mailbox, synchronous.
+int q_copy(void *dst, const void *src, size_t n, hipStream_t s);
+// q_bytes(dst, v, n, s): the n <= 8 low bytes of v (little endian) to device dst, by a kernel
+int q_bytes(void *dst, uint64_t v, uint32_t n, hipStream_t s);
 int mailbox(DeviceCtx *c, size_t n, void **p);
-// readback(c, dst, src, n, s): n bytes from the device to dst through the
-// mailbox, synchronous (s is synchronized)
 int readback(DeviceCtx *c, void *h_dst, const void *d_src, size_t n, hipStream_t s);
 // Host output buffer the caller frees with zt_free (large ones on huge pages;
 // pool = true: from the bounded host output pool, zt_api.cpp); host_release
