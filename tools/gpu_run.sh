@@ -24,7 +24,7 @@
 #   adapt:S1;S2;...   per-block depth sweep (ZT_DF_ADAPT settings) (adapt.log)
 #   regprobe          hipHostRegister vs pack of C4-sized buffers (regprobe.log)
 #   lib=PATH          later steps load libzt from PATH (ZT_LIB); lib= resets
-#   env=K=V           later steps see K=V
+#   env=K=V           later steps see K=V; unenv=K removes K
 set -e
 TAG=$1; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -72,6 +72,7 @@ for step in "$@"; do
     lib=) unset ZT_LIB ;;
     lib=*) export ZT_LIB=$R/${step#lib=} ;;
     env=*) export "${step#env=}" ;;
+    unenv=*) unset "${step#unenv=}" ;;
     *) echo "gpu_run: unknown step $step" >&2; exit 2 ;;
   esac
 done

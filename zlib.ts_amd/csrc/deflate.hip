@@ -2880,8 +2880,8 @@ int deflate_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t halo, in
   {
     void *mb;
     ZT_TRY(mailbox(c, 16, &mb));
-    ZT_TRY(q_copy(mb, off + G.nblocks, sizeof total, s));
-    ZT_TRY(q_copy((uint8_t *)mb + 8, P.nstore, 8, s));
+    ZT_TRY(x_copy(mb, off + G.nblocks, sizeof total, s));
+    ZT_TRY(x_copy((uint8_t *)mb + 8, P.nstore, 8, s));
     ZT_HIP(hipStreamSynchronize(s));
     memcpy(&total, mb, 8);
     memcpy(nst, (uint8_t *)mb + 8, 8);
@@ -3000,8 +3000,8 @@ int deflate_batch_dev_run(DeviceCtx *c, const uint8_t *d_in, size_t count, const
     void *mb;
     const size_t bb = boff.size() * 8;
     ZT_TRY(mailbox(c, bb + 8, &mb));
-    ZT_TRY(q_copy(mb, d_off, bb, s));
-    ZT_TRY(q_copy((uint8_t *)mb + bb, P.nstore, 8, s));
+    ZT_TRY(x_copy(mb, d_off, bb, s));
+    ZT_TRY(x_copy((uint8_t *)mb + bb, P.nstore, 8, s));
     ZT_HIP(hipStreamSynchronize(s));
     memcpy(boff.data(), mb, bb);
     memcpy(nst, (uint8_t *)mb + bb, 8);

@@ -446,16 +446,8 @@ static int inflate_raw_pipelined(DeviceCtx *c, const uint8_t *in, size_t n, size
   double ratio0 = 0;   // output bytes per input byte of piece 0
   size_t eip_last = 0;
   PipeOut po;
-  static const bool eager = getenv("ZT_INF_EAGER") != nullptr;  // (A/B hook: the host output allocated up front, 4x)
-  if (eager) {
-    po.base = host_out(cap, true);
-    po.cap = cap;
-    if (!po.base) return set_error(ZT_E_NOMEM, "host allocation failed");
-  }
   po.cap_fn = [&] { return (size_t)(ratio0 * 1.25 * (double)m) + (16u << 20); };
-  const int rc = pipeline_h2d_d2h(
-      c, np, [&](size_t i) { return PipePiece{in + cut[i], d_piece(i), cut[i + 1] - cut[i]}; },
-      [&](size_t i, const void **d_res, size_t *n_res) -> int {
+  auto compute = [&](size_t i, const void **d_res, size_t *n_res) -> int {
         const size_t len = cut[i + 1] - cut[i];
         const bool last = i + 1 == np;
         if (!last) {  // (by a kernel: no copy-engine command queued behind the pipeline's transfers)
@@ -474,7 +466,7 @@ static int inflate_raw_pipelined(DeviceCtx *c, const uint8_t *in, size_t n, size
             d_o = static_cast<uint8_t *>(d_big) + off;
             ocap = std::min(want, cap - off);
           } else {  // the overflow ring
-            if (ring0 == np) ring0 = i;
+            if (ring0 == np) ring0 = po.drain_from = i;
             const size_t r = (i - ring0) % kRing;
             if (i - ring0 >= kRing) ZT_TRY(po.drain(i - kRing));
             void *p;
@@ -502,8 +494,9 @@ static int inflate_raw_pipelined(DeviceCtx *c, const uint8_t *in, size_t n, size
           return ZT_OK;
         }
         return set_error(ZT_E_INTERNAL, "pipelined inflate: piece output did not settle");
-      },
-      po);
+      };
+  auto input = [&](size_t i) { return PipePiece{in + cut[i], d_piece(i), cut[i + 1] - cut[i]}; };
+  const int rc = pipeline_h2d_d2h(c, np, input, compute, po);
   if (rc) {  // (every copy has finished: the buffer can go)
     host_discard(po.base);
     return 1;

@@ -84,77 +84,105 @@ __device__ __forceinline__ uint32_t ldw(g_u32 *a32, int64_t wi, uint64_t lo, uin
 // HDIST <= 29.  Stage B per survivor: the HCLEN code-length code lengths form
 // a complete prefix code.  Stored blocks: LEN = ~NLEN at a byte whose
 // predecessor's top bits are zero padding.
+// Each workgroup takes FB_ITER spans of 256 dwords and gathers its stage-B
+// survivors in LDS: one atomic on the shared counter per workgroup (one per
+// wave serialised at the counter's L2 slice: 1.35 ms of a 64 MiB stream's
+// general decode, about one survivor per wave).
+constexpr int FB_ITER = 8;
+constexpr int FB_LOCAL = 1024;  // survivors a workgroup gathers (more: per-wave atomics)
 __global__ __launch_bounds__(256) void find_blocks(const uint8_t *in, uint64_t n, uint64_t index, uint64_t w_first,
                                                    uint64_t nw, uint64_t *listb, uint32_t *cntb, uint64_t *list,
                                                    uint32_t *cnt) {
-  // (every lane runs to the end: the appends are wave-aggregated)
-  const uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  __shared__ uint64_t loc[FB_LOCAL];
+  __shared__ uint32_t nloc, gbase;
+  if (threadIdx.x == 0) nloc = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
   const uintptr_t a = reinterpret_cast<uintptr_t>(in);
   g_u32 *a32 = (g_u32 *)(a & ~uintptr_t(15));
   const uint64_t lo = a & 15, hi = lo + n;
-  const int64_t wi = (int64_t)(w_first + (k < nw ? k : nw));
-  const uint32_t wm = ldw(a32, wi - 1, lo, hi);
-  const uint32_t w0 = ldw(a32, wi, lo, hi), w1 = ldw(a32, wi + 1, lo, hi);
-  const uint32_t w2 = ldw(a32, wi + 2, lo, hi), w3 = ldw(a32, wi + 3, lo, hi);
-  auto S = [&](int s) -> uint32_t { return __builtin_amdgcn_alignbit(w1, w0, s); };
-  uint32_t M = ~S(1) & S(2);
-  M &= ~(S(4) & S(5) & S(6) & S(7));
-  M &= ~(S(9) & S(10) & S(11) & S(12));
-  const uint64_t base = (uint64_t)wi * 32;
   const uint64_t pmin = (lo + index) * 8;
   const uint64_t pmax = hi * 8 >= 17 ? hi * 8 - 17 : 0;  // a header needs >= 17 bits
-  if (k >= nw) M = 0;
-  if (base < pmin) M = (pmin - base >= 32) ? 0u : (M & (0xFFFFFFFFu << (pmin - base)));
-  if (base + 32 > pmax) M = (base >= pmax) ? 0u : (M & (0xFFFFFFFFu >> (32 - (pmax - base))));
-  uint32_t B = 0;  // survivors of stage B
-  while (M) {
-    const int j = __builtin_ctz(M);
-    M &= M - 1;
-    const uint32_t x0 = j ? __builtin_amdgcn_alignbit(w1, w0, j) : w0;
-    const uint32_t x1 = j ? __builtin_amdgcn_alignbit(w2, w1, j) : w1;
-    const uint32_t x2 = j ? __builtin_amdgcn_alignbit(w3, w2, j) : w2;
-    const uint32_t ncl = ((x0 >> 13) & 15) + 4;
-    const uint64_t cl = (((uint64_t)x1 << 32 | x0) >> 17) | ((uint64_t)x2 << 47);
-    uint32_t kraft = 0;
+  for (int it = 0; it < FB_ITER; ++it) {
+    // (every lane runs to the end: the appends are wave-aggregated)
+    const uint64_t k = ((uint64_t)blockIdx.x * FB_ITER + it) * 256 + threadIdx.x;
+    const int64_t wi = (int64_t)(w_first + (k < nw ? k : nw));
+    const uint32_t wm = ldw(a32, wi - 1, lo, hi);
+    const uint32_t w0 = ldw(a32, wi, lo, hi), w1 = ldw(a32, wi + 1, lo, hi);
+    const uint32_t w2 = ldw(a32, wi + 2, lo, hi), w3 = ldw(a32, wi + 3, lo, hi);
+    auto S = [&](int sh) -> uint32_t { return __builtin_amdgcn_alignbit(w1, w0, sh); };
+    uint32_t M = ~S(1) & S(2);
+    M &= ~(S(4) & S(5) & S(6) & S(7));
+    M &= ~(S(9) & S(10) & S(11) & S(12));
+    const uint64_t base = (uint64_t)wi * 32;
+    if (k >= nw) M = 0;
+    if (base < pmin) M = (pmin - base >= 32) ? 0u : (M & (0xFFFFFFFFu << (pmin - base)));
+    if (base + 32 > pmax) M = (base >= pmax) ? 0u : (M & (0xFFFFFFFFu >> (32 - (pmax - base))));
+    uint32_t B = 0;  // survivors of stage B
+    while (M) {
+      const int j = __builtin_ctz(M);
+      M &= M - 1;
+      const uint32_t x0 = j ? __builtin_amdgcn_alignbit(w1, w0, j) : w0;
+      const uint32_t x1 = j ? __builtin_amdgcn_alignbit(w2, w1, j) : w1;
+      const uint32_t x2 = j ? __builtin_amdgcn_alignbit(w3, w2, j) : w2;
+      const uint32_t ncl = ((x0 >> 13) & 15) + 4;
+      const uint64_t cl = (((uint64_t)x1 << 32 | x0) >> 17) | ((uint64_t)x2 << 47);
+      uint32_t kraft = 0;
 #pragma unroll
-    for (uint32_t i = 0; i < 19; ++i) {
-      const uint32_t l = (uint32_t)(cl >> (3 * i)) & 7;
-      kraft += (i < ncl && l) ? (128u >> l) : 0u;
+      for (uint32_t i = 0; i < 19; ++i) {
+        const uint32_t l = (uint32_t)(cl >> (3 * i)) & 7;
+        kraft += (i < ncl && l) ? (128u >> l) : 0u;
+      }
+      if (kraft == 128) B |= 1u << j;
     }
-    if (kraft == 128) B |= 1u << j;
-  }
-  // one atomic per wave: survivors appended at a wave-reserved range
-  const uint32_t nbk = __popc(B);
-  uint32_t pre = nbk;
-  const int lane = threadIdx.x & 63;
+    // survivors into the workgroup's LDS list (one LDS atomic per wave), or
+    // when it is full straight to the global list
+    const uint32_t nbk = __popc(B);
+    uint32_t pre = nbk;
 #pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t v = __shfl_up(pre, off, 64);
-    if (lane >= off) pre += v;
-  }
-  const uint32_t wtot = __shfl(pre, 63, 64);
-  uint32_t wbase = 0;
-  if (lane == 63 && wtot) wbase = atomicAdd(cntb, wtot);
-  wbase = __shfl(wbase, 63, 64);
-  uint32_t q = wbase + pre - nbk;
-  while (B) {
-    const int j = __builtin_ctz(B);
-    B &= B - 1;
-    if (q < kMaxCandB) listb[q] = base + j;
-    ++q;
-  }
-  // stored LEN fields at bytes 4 wi + j
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t v = __shfl_up(pre, off, 64);
+      if (lane >= off) pre += v;
+    }
+    const uint32_t wtot = __shfl(pre, 63, 64);
+    if (wtot) {
+      uint32_t wb = 0;
+      if (lane == 63) wb = atomicAdd(&nloc, wtot);
+      wb = __shfl(wb, 63, 64);
+      const bool local = wb + wtot <= (uint32_t)FB_LOCAL;
+      uint32_t gb = 0;
+      if (!local && lane == 63) gb = atomicAdd(cntb, wtot);
+      gb = __shfl(gb, 63, 64);
+      uint32_t q = pre - nbk;
+      while (B) {
+        const int j = __builtin_ctz(B);
+        B &= B - 1;
+        if (local)
+          loc[wb + q] = base + j;
+        else if (gb + q < kMaxCandB)
+          listb[gb + q] = base + j;
+        ++q;
+      }
+    }
+    // stored LEN fields at bytes 4 wi + j
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const uint64_t q = (uint64_t)wi * 4 + j;
-    if (k >= nw || q < lo + index + 1 || q + 4 > hi) continue;
-    const uint32_t x = j ? __builtin_amdgcn_alignbyte(w1, w0, j) : w0;
-    const uint32_t prevb = j ? (w0 >> (8 * (j - 1))) & 0xFF : wm >> 24;
-    if (((x ^ (x >> 16)) & 0xFFFF) == 0xFFFF && (prevb >> 6) == 0) {
-      const uint32_t c = atomicAdd(cnt, 1u);
-      if (c < kMaxCand) list[c] = ((q - lo) * 8) << 17 | (uint64_t)(x & 0xFFFF) << 1 | 1;
+    for (int j = 0; j < 4; ++j) {
+      const uint64_t q = (uint64_t)wi * 4 + j;
+      if (k >= nw || q < lo + index + 1 || q + 4 > hi) continue;
+      const uint32_t x = j ? __builtin_amdgcn_alignbyte(w1, w0, j) : w0;
+      const uint32_t prevb = j ? (w0 >> (8 * (j - 1))) & 0xFF : wm >> 24;
+      if (((x ^ (x >> 16)) & 0xFFFF) == 0xFFFF && (prevb >> 6) == 0) {
+        const uint32_t c = atomicAdd(cnt, 1u);
+        if (c < kMaxCand) list[c] = ((q - lo) * 8) << 17 | (uint64_t)(x & 0xFFFF) << 1 | 1;
+      }
     }
   }
+  __syncthreads();
+  const uint32_t nl = nloc < (uint32_t)FB_LOCAL ? nloc : (uint32_t)FB_LOCAL;
+  if (threadIdx.x == 0) gbase = nl ? atomicAdd(cntb, nl) : 0u;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < nl; i += 256)
+    if (gbase + i < kMaxCandB) listb[gbase + i] = loc[i];
 }
 
 // Stage C: one lane per survivor -- the dynamic header decoded in full with a
@@ -889,7 +917,8 @@ int inflate_general_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t inde
   uint64_t *d_list = reinterpret_cast<uint64_t *>(static_cast<uint8_t *>(d_c) + 256 + listb_bytes);
   ZT_TRY(timing_begin(c, s, 2));
   ZT_HIP(hipMemsetAsync(d_cnt, 0, 8, s));
-  find_blocks<<<(uint32_t)((nw + 255) / 256), 256, 0, s>>>(d_in, n, index, w_first, nw, d_listb, d_cnt, d_list,
+  find_blocks<<<(uint32_t)((nw + 256 * FB_ITER - 1) / (256 * FB_ITER)), 256, 0, s>>>(d_in, n, index, w_first, nw,
+                                                                                    d_listb, d_cnt, d_list,
                                                            d_cnt + 1);
   ZT_HIP(hipGetLastError());
   uint32_t cnts[2];
@@ -1058,8 +1087,8 @@ int inflate_general_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t inde
       void *mb;
       const size_t rb = units * sizeof(GenResult), lb = units * sizeof(GenLink);
       ZT_TRY(mailbox(c, rb + lb, &mb));
-      ZT_TRY(q_copy(mb, d_res, rb, s));
-      ZT_TRY(q_copy((uint8_t *)mb + rb, d_link, lb, s));
+      ZT_TRY(x_copy(mb, d_res, rb, s));
+      ZT_TRY(x_copy((uint8_t *)mb + rb, d_link, lb, s));
       ZT_HIP(hipStreamSynchronize(s));
       memcpy(res.data(), mb, rb);
       memcpy(link.data(), (uint8_t *)mb + rb, lb);
@@ -1311,8 +1340,8 @@ int inflate_general_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t inde
   {
     void *mb;
     ZT_TRY(mailbox(c, (chain.size() + segs.size()) * 4, &mb));
-    ZT_TRY(q_copy(mb, d_ust, chain.size() * 4, s));
-    ZT_TRY(q_copy((uint8_t *)mb + chain.size() * 4, d_st, segs.size() * 4, s));
+    ZT_TRY(x_copy(mb, d_ust, chain.size() * 4, s));
+    ZT_TRY(x_copy((uint8_t *)mb + chain.size() * 4, d_st, segs.size() * 4, s));
     ZT_HIP(hipStreamSynchronize(s));
     memcpy(ust.data(), mb, chain.size() * 4);
     memcpy(sst.data(), (uint8_t *)mb + chain.size() * 4, segs.size() * 4);

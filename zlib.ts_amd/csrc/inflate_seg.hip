@@ -578,9 +578,9 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
     ZT_TRY(mailbox(c, 24, &mb));
     uint64_t *m64 = static_cast<uint64_t *>(mb);
     m64[1] = m64[2] = 0;
-    ZT_TRY(q_copy(&m64[0], d_ttot, 8, s));
-    ZT_TRY(q_copy(&m64[1], d_pos + cnt, 4, s));
-    ZT_TRY(q_copy(&m64[2], d_ttot + 2, 4, s));
+    ZT_TRY(x_copy(&m64[0], d_ttot, 8, s));
+    ZT_TRY(x_copy(&m64[1], d_pos + cnt, 4, s));
+    ZT_TRY(x_copy(&m64[2], d_ttot + 2, 4, s));
     ZT_HIP(hipStreamSynchronize(s));
     for (int k = 0; k < 3; ++k) tot_h[k] = m64[k];
   }
@@ -693,7 +693,7 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
     ZT_TRY(timing_end(c, s, 2));
     // back in one copy: the chain summary and every status
     uint8_t *hb = pin + meta_a;
-    ZT_TRY(q_copy(hb, d_ust, ust_bytes + st_bytes + sizeof(ChainInfo) + 4, s));
+    ZT_TRY(x_copy(hb, d_ust, ust_bytes + st_bytes + sizeof(ChainInfo) + 4, s));
     ZT_HIP(hipStreamSynchronize(s));
     IT("resolved (device chain)");
     const ChainInfo info = *reinterpret_cast<const ChainInfo *>(hb + ust_bytes + st_bytes);
@@ -718,10 +718,10 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   }
 host_walk:
   TokResult *res = reinterpret_cast<TokResult *>(pin + restart_bytes);
-  ZT_TRY(q_copy(pin, d_restart, nsync, s));
-  ZT_TRY(q_copy(res, d_res, units * sizeof(TokResult), s));
+  ZT_TRY(x_copy(pin, d_restart, nsync, s));
+  ZT_TRY(x_copy(res, d_res, units * sizeof(TokResult), s));
   const uint64_t *tok_off = reinterpret_cast<const uint64_t *>(pin + restart_bytes + res_bytes);
-  ZT_TRY(q_copy(pin + restart_bytes + res_bytes, d_off, units * 8, s));
+  ZT_TRY(x_copy(pin + restart_bytes + res_bytes, d_off, units * 8, s));
   ZT_HIP(hipStreamSynchronize(s));
   IT("tokenized");
   if (check) {
@@ -855,8 +855,8 @@ host_walk:
   int32_t *h_st = h_ust + align256(units_max * 4) / 4;
   memcpy(h_cu, chain.data(), chain.size() * sizeof(ChainUnit));
   memcpy(h_sj, segs.data(), segs.size() * sizeof(SegJob));
-  ZT_TRY(q_copy(d_cu, h_cu, chain.size() * sizeof(ChainUnit), s));
-  ZT_TRY(q_copy(d_sj, h_sj, segs.size() * sizeof(SegJob), s));
+  ZT_TRY(x_copy(d_cu, h_cu, chain.size() * sizeof(ChainUnit), s));
+  ZT_TRY(x_copy(d_sj, h_sj, segs.size() * sizeof(SegJob), s));
   ResolveParams rp;
   rp.tokens = static_cast<const uint32_t *>(d_tok);
   rp.units = d_cu;
@@ -872,8 +872,8 @@ host_walk:
   IT("chain built");
   ZT_TRY(resolve_segments_dev(rp, s));
   ZT_TRY(timing_end(c, s, 2));
-  ZT_TRY(q_copy(h_ust, d_ust, chain.size() * 4, s));
-  ZT_TRY(q_copy(h_st, d_st, segs.size() * 4, s));
+  ZT_TRY(x_copy(h_ust, d_ust, chain.size() * 4, s));
+  ZT_TRY(x_copy(h_st, d_st, segs.size() * 4, s));
   ZT_HIP(hipStreamSynchronize(s));
   IT("resolved");
   ZT_TRY(timing_collect(c, &c->times.inflate_ms, &c->times.inflate_launches, 2));

@@ -367,11 +367,18 @@ int mailbox(DeviceCtx *c, size_t n, void **p) {
   return ZT_OK;
 }
 
+int x_copy(void *dst, const void *src, size_t n, hipStream_t s) {
+  static const bool qc = getenv("ZT_QCOPY") != nullptr;
+  if (qc) return q_copy(dst, src, n, s);
+  if (n) ZT_HIP(hipMemcpyAsync(dst, src, n, hipMemcpyDefault, s));
+  return ZT_OK;
+}
+
 int readback(DeviceCtx *c, void *h_dst, const void *d_src, size_t n, hipStream_t s) {
   if (!n) return ZT_OK;
   void *mb;
   ZT_TRY(mailbox(c, n, &mb));
-  ZT_TRY(q_copy(mb, d_src, n, s));
+  ZT_TRY(x_copy(mb, d_src, n, s));
   ZT_HIP(hipStreamSynchronize(s));
   memcpy(h_dst, mb, n);
   return ZT_OK;
@@ -596,7 +603,7 @@ int pipeline_h2d_d2h(DeviceCtx *c, size_t np, const std::function<PipePiece(size
         k += nch;
       }
       total += n;
-      ZT_HIP(hipEventRecord(drained[i], c->dn));
+      if (i >= out.drain_from) ZT_HIP(hipEventRecord(drained[i], c->dn));
       std::lock_guard<std::mutex> lk(mu);
       downloaded = i + 1;
       cv.notify_all();
@@ -604,6 +611,7 @@ int pipeline_h2d_d2h(DeviceCtx *c, size_t np, const std::function<PipePiece(size
     return ZT_OK;
   };
   out.drain = [&](size_t j) -> int {
+    if (j < out.drain_from) return set_error(ZT_E_INTERNAL, "pipeline: drain of a piece before drain_from");
     {
       std::unique_lock<std::mutex> lk(mu);
       cv.wait(lk, [&] { return downloaded > j || err; });

@@ -87,17 +87,17 @@ int scratch(DeviceCtx *c, int slot, size_t bytes, void **ptr);
 // Grow-only pinned host staging buffer `slot` (0 or 1) of at least `bytes`.
 int pinned(DeviceCtx *c, size_t bytes, void **ptr, int slot = 0);
 // Small transfers between the host and the device (counts, per-unit
-// results, chain tables) are made by a kernel on the calling stream over
-// pinned host memory the GPU addresses directly, not by the copy engines:
-// hipMemcpyAsync of a few bytes queues behind the large copies the host
-// pipelines keep on the engines (their uploads and downloads, 32-180 MB
-// each) and waited 1-4 ms per transfer there, and a pageable destination
-// adds a staging copy.  q_copy(dst, src, n, s): the kernel copy (either end
-// device or pinned host memory).  mailbox(c, n): a pinned, coherent region of
+// results, chain tables) go through pinned memory: a pageable destination
+// adds a staging copy inside the runtime.  q_copy(dst, src, n, s): a kernel
+// copy (either end device or pinned host memory).  mailbox(c, n): a pinned, coherent region of
 // >= n bytes (pinned slot 8), valid until the next mailbox call (one user at
 // a time: the context's caller thread).  readback(c, dst, src, n, s): n bytes
 // from the device to any host dst through the mailbox, synchronous.
 int q_copy(void *dst, const void *src, size_t n, hipStream_t s);
+// small transfer into / out of pinned memory: the copy engines
+// (hipMemcpyAsync), or with ZT_QCOPY=1 q_copy (A/B: measured slower inside
+// the host pipelines, gpurun_out/r06t)
+int x_copy(void *dst, const void *src, size_t n, hipStream_t s);
 // q_bytes(dst, v, n, s): the n <= 8 low bytes of v (little endian) to device dst, by a kernel
 int q_bytes(void *dst, uint64_t v, uint32_t n, hipStream_t s);
 int mailbox(DeviceCtx *c, size_t n, void **p);
@@ -407,8 +407,13 @@ struct PipeOut {
   size_t total = 0;  // out: bytes written
   // set by the pipeline for compute(i): drain(j), j < i, makes the compute
   // stream wait until piece j's result has left the device (before compute
-  // reuses its device buffer); waits on the host until that copy is issued
+  // reuses its device buffer); waits on the host until that copy is issued.
+  // Only pieces from drain_from on can be drained: compute sets it (before
+  // it returns piece drain_from) when it starts reusing buffers -- an event
+  // recorded behind every download cost the inflate pipeline ~3 ms per GiB
+  // (gpurun_out/r06u).
   std::function<int(size_t)> drain;
+  size_t drain_from = SIZE_MAX;
 };
 int pipeline_h2d_d2h(DeviceCtx *c, size_t np, const std::function<PipePiece(size_t)> &input,
                      const std::function<int(size_t, const void **d_res, size_t *n_res)> &compute, PipeOut &out);
