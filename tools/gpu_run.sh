@@ -18,10 +18,12 @@
 #   api               host-API inflate time (appends)         (api.log)
 #   infprof           rocprof kernel stats of infgen          (infgen_kernel_stats.csv)
 #   infgen[:MiB]      foreign-stream inflate timing           (inflate_general_time.json)
+#   infgenq           infgen, one summary line (appends)      (infgen.log)
 #   kinds             per-generator deflate / inflate times   (kinds.log)
 #   digest            stream digests (levels 6 / 1 / 9)       (digest.log)
 #   node              Node facade bench (tools/node_bench.mjs) (node.log)
 #   adapt:S1;S2;...   per-block depth sweep (ZT_DF_ADAPT settings) (adapt.log)
+#   dftime            match-kernel cycle split (ab_dftime build)  (dftime.log)
 #   regprobe          hipHostRegister vs pack of C4-sized buffers (regprobe.log)
 #   lib=PATH          later steps load libzt from PATH (ZT_LIB); lib= resets
 #   env=K=V           later steps see K=V; unenv=K removes K
@@ -63,11 +65,13 @@ for step in "$@"; do
     api) timeout -k 10 300 python3 tools/api_inflate_time.py >> $O/api.log 2>&1; echo "${ZT_LIB:-HEAD} $(tail -1 $O/api.log)" ;;
     infprof) prof infgen 600 -- python3 $R/tools/inflate_general_time.py 64 ;;
     infgen) timeout -k 10 600 python3 -u tools/inflate_general_time.py 64 $O/inflate_general_time.json > $O/infgen.log 2>&1; tail -1 $O/infgen.log | cut -c1-600 ;;
+    infgenq) timeout -k 10 600 python3 -u tools/inflate_general_time.py 64 $O/inflate_general_time.json >> $O/infgen.log 2>&1; echo "$(env | grep ZT_GEN | tr '\n' ' ') $(tail -1 $O/infgen.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print({k: (v["device"]["wall_ms"], v["device"]["passes_per_call"], v["host_api_GiBps"]) for k, v in d.items() if isinstance(v, dict)})')" ;;
     infgen:*) timeout -k 10 600 python3 -u tools/inflate_general_time.py ${step#infgen:} $O/inflate_general_time.json > $O/infgen.log 2>&1; tail -1 $O/infgen.log | cut -c1-600 ;;
     kinds) timeout -k 10 300 python3 tools/kind_time.py > $O/kinds.log 2>&1; tail -8 $O/kinds.log ;;
     digest) DF_LEVELS=6,1,9 timeout -k 10 300 python3 tools/df_digest.py wordsalad structured mixed > $O/digest.log 2>&1; grep -E 'L6|L1|L9' $O/digest.log ;;
     node) timeout -k 10 300 node --expose-gc tools/node_bench.mjs > $O/node.log 2>&1; tail -1 $O/node.log ;;
     adapt:*) IFS=';' read -ra A <<< "${step#adapt:}"; timeout -k 10 900 python3 -u tools/adapt_sweep.py "" "${A[@]}" > $O/adapt.log 2>&1; grep '^\[' $O/adapt.log ;;
+    dftime) ZT_LIB=$R/zlib.ts_amd/build/ab_dftime/libzt.so timeout -k 10 300 python3 tools/df_time.py wordsalad structured > $O/dftime.log 2>&1; grep sub-chunk $O/dftime.log ;;
     regprobe) timeout -k 10 300 tools/micro/host_register_probe > $O/regprobe.log 2>&1; cat $O/regprobe.log ;;
     lib=) unset ZT_LIB ;;
     lib=*) export ZT_LIB=$R/${step#lib=} ;;

@@ -195,7 +195,7 @@ int batch_grouped(DeviceCtx *c, const uint8_t *const *in, const std::vector<size
       const double t0 = stage_now();
       parallel_copy(nb, [&](size_t j) {
         const size_t k = gk[g] + j;
-        memcpy(st + off[k] - b, in[work[k]], len[k]);
+        copy_to_staging(st + off[k] - b, in[work[k]], len[k]);
         memset(st + off[k] - b + len[k], 0, round_blk(len[k]) - len[k]);
       }, gend(g) - b);
       tm.pack_ms += stage_now() - t0;  // (this thread only)
@@ -332,7 +332,7 @@ int batch_on_device(int dev, const uint8_t *const *in, const size_t *n, const st
   uint8_t *stage = static_cast<uint8_t *>(h_stage);
   const double t_pack = stage_now();
   parallel_copy(m, [&](size_t k) {
-    memcpy(stage + off[k], in[work[k]], len[k]);
+    copy_to_staging(stage + off[k], in[work[k]], len[k]);
     memset(stage + off[k] + len[k], 0, round_blk(len[k]) - len[k]);
   }, in_bytes);
   tm.pack_ms += stage_now() - t_pack;
@@ -389,12 +389,59 @@ int batch_on_device(int dev, const uint8_t *const *in, const size_t *n, const st
     if (int rc = deflate_batch_dev_run(c, (const uint8_t *)d_in, m, off.data(), len.data(), ct, lv,
                                        (uint8_t *)d_out, oo.data(), d_scr, ss, c->stream))
       return fail(rc);
-    // the staged input has been consumed (the pipeline waited for its stream)
-    void *h_out;
-    if (int rc = pinned(c, oo[m], &h_out, 0)) return fail(rc);
-    ZT_HIP(hipMemcpyAsync(h_out, d_out, oo[m], hipMemcpyDeviceToHost, c->stream));
-    ZT_HIP(hipStreamSynchronize(c->stream));
-    body_host = static_cast<uint8_t *>(h_out);
+    // The members are framed on the device (prefix | stream | trailer, at
+    // their slab offsets) and come back with one copy -- straight into the
+    // slab when it is a registered pool buffer (a caller batching again after
+    // freeing the last outputs): the host only lays the slab out.  Host
+    // framing (the slab filled from a staged copy of the streams) was a
+    // quarter of a device thread's host time on a node's worth of devices
+    // (tools/c4_host_stages.py).
+    const double t_frame = stage_now();
+    const uint32_t plen = (uint32_t)fr.prefix.size(), tl = (uint32_t)fr.trailer;
+    std::vector<FrameItem> fi(m);
+    std::vector<size_t> soff(m);
+    size_t tot = 0;
+    for (size_t k = 0; k < m; ++k) {
+      soff[k] = tot;
+      fi[k] = FrameItem{oo[k], tot, (uint32_t)(oo[k + 1] - oo[k]), (uint32_t)len[k]};
+      tot += (plen + (oo[k + 1] - oo[k]) + tl + 64) & ~size_t(63);
+    }
+    const size_t fr_bytes = (tot + 255) & ~size_t(255), it_bytes = (m * sizeof(FrameItem) + 255) & ~size_t(255);
+    void *d_fr;
+    if (int rc = scratch(c, 27, fr_bytes + it_bytes + plen + 256, &d_fr)) return fail(rc);
+    uint8_t *d_framed = static_cast<uint8_t *>(d_fr);
+    FrameItem *d_items = reinterpret_cast<FrameItem *>(d_framed + fr_bytes);
+    uint8_t *d_prefix = d_framed + fr_bytes + it_bytes;
+    ZT_HIP(hipMemcpyAsync(d_items, fi.data(), m * sizeof(FrameItem), hipMemcpyHostToDevice, c->stream));
+    if (plen) ZT_HIP(hipMemcpyAsync(d_prefix, fr.prefix.data(), plen, hipMemcpyHostToDevice, c->stream));
+    if (sums) {  // (the trailers need the checksums from the second stream)
+      ZT_HIP(hipEventRecord(c->aux_ev, c->aux));
+      ZT_HIP(hipStreamWaitEvent(c->stream, c->aux_ev, 0));
+    }
+    if (int rc = frame_members_dev(d_items, (uint32_t)m, d_prefix, plen,
+                                   fr.kind == Framing::GZIP ? 8u : fr.kind == Framing::ZLIB ? 4u : 0u,
+                                   static_cast<const uint8_t *>(d_out), static_cast<const uint32_t *>(d_sums),
+                                   d_framed, c->stream))
+      return fail(rc);
+    uint8_t *slab = slab_out(tot, m, true);
+    if (!slab) return fail(set_error(ZT_E_NOMEM, "host allocation failed"));
+    const bool direct = host_direct(slab, tot);
+    tm.frame_ms += stage_now() - t_frame;
+    if (direct) {  // (DMA time, not host work: like the upload, outside the stage timers)
+      ZT_HIP(hipMemcpyAsync(slab, d_framed, tot, hipMemcpyDeviceToHost, c->stream));
+      ZT_HIP(hipStreamSynchronize(c->stream));
+    } else {
+      const double t_dl = stage_now();
+      if (int rc = download(c, slab, d_framed, tot, c->stream)) return fail(rc);
+      tm.frame_ms += stage_now() - t_dl;  // (staged: host copies)
+    }
+    ZT_HIP(hipStreamSynchronize(c->aux));
+    for (size_t k = 0; k < m; ++k) {
+      out[work[k]] = slab + soff[k];
+      out_len[work[k]] = plen + (oo[k + 1] - oo[k]) + tl;
+    }
+    tm.out_bytes += oo[m];
+    return ZT_OK;
   }
   ZT_HIP(hipStreamSynchronize(c->aux));
   int first_rc = ZT_OK;
@@ -450,7 +497,16 @@ int run_batch(const uint8_t *const *in, const size_t *n, size_t count, int ct, i
   } else {
     std::vector<std::thread> th;
     for (size_t d = 0; d < nd; ++d)
-      th.emplace_back([&, d] { rc[d] = batch_on_device(devs[d], in, n, share[d], ct, lv, fr, out, out_len, &err[d]); });
+      th.emplace_back([&, d] {
+        // the host's copy threads split between the device threads (8 per
+        // device thread put 64 on one GPU's 16-thread CPU share with 8
+        // devices; 32 in all packed fastest: slowest device's host stages
+        // 10.9 GiB/s with 16, 13.3 with 32, gpurun_out/r06ab);
+        // ZT_BATCH_COPY_THREADS overrides the total
+        static const size_t total = getenv("ZT_BATCH_COPY_THREADS") ? (size_t)atoi(getenv("ZT_BATCH_COPY_THREADS")) : 32;
+        set_copy_threads(std::max<size_t>(2, total / nd));
+        rc[d] = batch_on_device(devs[d], in, n, share[d], ct, lv, fr, out, out_len, &err[d]);
+      });
     for (auto &t : th) t.join();
   }
   int first = ZT_OK;
@@ -529,7 +585,7 @@ int zt_crc32_batch(const uint8_t *const *in, const size_t *n, size_t count, uint
   ZT_TRY(scratch(c, 0, tot + 64, &d_in));
   ZT_TRY(pinned(c, tot + 64, &h, 0));
   uint8_t *stage = static_cast<uint8_t *>(h);
-  parallel_copy(count, [&](size_t i) { if (n[i]) memcpy(stage + off[i], in[i], n[i]); }, tot);
+  parallel_copy(count, [&](size_t i) { copy_to_staging(stage + off[i], in[i], n[i]); }, tot);
   ZT_HIP(hipMemcpyAsync(d_in, stage, tot ? tot : 1, hipMemcpyHostToDevice, c->stream));
   ZT_TRY(scratch(c, 18, 8 * count, &d_sums));
   ZT_TRY(checksums_batch_dev(c, (const uint8_t *)d_in, count, off.data(), len.data(), (uint32_t *)d_sums, c->stream));

@@ -337,7 +337,7 @@ static int inflate_host_batch(const uint8_t *const *in, const size_t *n, const s
     ZT_TRY(pinned(c, in_total, &h));
     uint8_t *stage = (uint8_t *)h;
     BT("pack start");
-    parallel_copy(count, [&](size_t i) { if (n[i]) memcpy(stage + in_off[i], in[i], n[i]); }, in_total);
+    parallel_copy(count, [&](size_t i) { copy_to_staging(stage + in_off[i], in[i], n[i]); }, in_total);
     BT("pack done");
     ZT_HIP(hipMemcpyAsync(d_in, stage, in_total, hipMemcpyHostToDevice, c->stream));
   }

@@ -102,7 +102,55 @@ __global__ void q_bytes_kernel(uint8_t *dst, uint64_t v, uint32_t n) {
   if (threadIdx.x < n) dst[threadIdx.x] = (uint8_t)(v >> (8 * threadIdx.x));
 }
 
+// one workgroup per member: prefix, body, trailer (CRC-32 + ISIZE little
+// endian, or Adler-32 big endian)
+__global__ __launch_bounds__(256) void frame_members_kernel(const FrameItem *__restrict__ items,
+                                                            const uint8_t *__restrict__ prefix, uint32_t plen,
+                                                            uint32_t trailer, const uint8_t *__restrict__ body,
+                                                            const uint32_t *__restrict__ sums,
+                                                            uint8_t *__restrict__ out) {
+  const FrameItem it = items[blockIdx.x];
+  uint8_t *o = out + it.out_off;
+  for (uint32_t i = threadIdx.x; i < plen; i += 256) o[i] = prefix[i];
+  const uint8_t *b = body + it.body_off;
+  uint8_t *ob = o + plen;
+  // (body and destination offsets are arbitrary: dwords read unaligned by
+  // byte aligns from the source's aligned words)
+  const uint32_t n = it.body_len;
+  const uint32_t lead = (uint32_t)((4 - ((uintptr_t)ob & 3)) & 3) < n ? (uint32_t)((4 - ((uintptr_t)ob & 3)) & 3) : n;
+  for (uint32_t i = threadIdx.x; i < lead; i += 256) ob[i] = b[i];
+  const uint8_t *bs = b + lead;
+  uint32_t *od = reinterpret_cast<uint32_t *>(ob + lead);
+  const uint32_t nw = (n - lead) / 4;
+  const uint32_t sh = (uint32_t)((uintptr_t)bs & 3);
+  const uint32_t *sw = reinterpret_cast<const uint32_t *>(bs - sh);
+  for (uint32_t w = threadIdx.x; w < nw; w += 256) {
+    const uint32_t lo = sw[w], hi = sh ? sw[w + 1] : 0u;
+    od[w] = sh ? __builtin_amdgcn_alignbyte(hi, lo, sh) : lo;
+  }
+  for (uint32_t i = lead + 4 * nw + threadIdx.x; i < n; i += 256) ob[i] = b[i];
+  if (threadIdx.x == 0) {
+    uint8_t *t = ob + n;
+    if (trailer == 8) {
+      const uint32_t crc = sums[2 * blockIdx.x];
+      for (int k = 0; k < 4; ++k) t[k] = (uint8_t)(crc >> (8 * k));
+      for (int k = 0; k < 4; ++k) t[4 + k] = (uint8_t)(it.isize >> (8 * k));
+    } else if (trailer == 4) {
+      const uint32_t ad = sums[2 * blockIdx.x + 1];
+      for (int k = 0; k < 4; ++k) t[k] = (uint8_t)(ad >> (24 - 8 * k));
+    }
+  }
+}
+
 }  // namespace
+
+int frame_members_dev(const FrameItem *d_items, uint32_t count, const uint8_t *d_prefix, uint32_t plen,
+                      uint32_t trailer, const uint8_t *d_body, const uint32_t *d_sums, uint8_t *d_out, hipStream_t s) {
+  if (!count) return ZT_OK;
+  frame_members_kernel<<<count, 256, 0, s>>>(d_items, d_prefix, plen, trailer, d_body, d_sums, d_out);
+  ZT_HIP(hipGetLastError());
+  return ZT_OK;
+}
 
 int q_bytes(void *dst, uint64_t v, uint32_t n, hipStream_t s) {
   if (!n) return ZT_OK;

@@ -2,6 +2,7 @@
 //
 // Every entry point computes on the GPU.  There is deliberately no CPU
 // fallback: without a HIP device the calls fail with ZT_E_NO_DEVICE.
+#include <immintrin.h>
 #include <sys/mman.h>
 
 #include <algorithm>
@@ -299,9 +300,9 @@ struct Slab {
 static std::mutex g_slab_mu;
 static std::map<uintptr_t, Slab> g_slabs;
 
-uint8_t *slab_out(size_t total, size_t items) {
+uint8_t *slab_out(size_t total, size_t items, bool pool) {
   if (total == 0) total = 1;
-  uint8_t *b = host_out(total);
+  uint8_t *b = host_out(total, pool);
   if (!b) return nullptr;
   std::lock_guard<std::mutex> lk(g_slab_mu);
   g_slabs[(uintptr_t)b] = Slab{total, items};
@@ -392,17 +393,18 @@ static constexpr size_t kXferChunk = 32u << 20;
 
 // (fresh output pages fault in during the copy: 8 threads keep a 32 MiB
 // chunk's faults and copy under its DMA time; tools/micro/host_fault_probe)
+void copy_to_staging(void *dst, const void *src, size_t n);
 static void host_copy(void *dst, const void *src, size_t n) {
   const size_t nt = n >= (16u << 20) ? 8 : n >= (8u << 20) ? 4 : 1;
   if (nt == 1) {
-    memcpy(dst, src, n);
+    copy_to_staging(dst, src, n);
     return;
   }
   std::vector<std::thread> th;
   const size_t per = (n + nt - 1) / nt;
   for (size_t t = 0; t < nt; ++t) {
     const size_t a = t * per, b = std::min(n, a + per);
-    if (a < b) th.emplace_back([=] { memcpy((uint8_t *)dst + a, (const uint8_t *)src + a, b - a); });
+    if (a < b) th.emplace_back([=] { copy_to_staging((uint8_t *)dst + a, (const uint8_t *)src + a, b - a); });
   }
   for (auto &t : th) t.join();
 }
@@ -672,10 +674,53 @@ int pipeline_h2d_d2h(DeviceCtx *c, size_t np, const std::function<PipePiece(size
   return ZT_OK;
 }
 
+// Copy into staging that only the DMA engine reads back: non-temporal
+// (streaming) stores skip the read-for-ownership of every destination line
+// and leave the caches to the source -- one read and one write of memory
+// traffic per byte instead of two reads and a write, which is what several
+// device threads packing at once share (config C4 on 8 GPUs).  AVX2 where
+// the host has it, memcpy otherwise; an sfence at the end orders the stores
+// before the caller issues the DMA.
+__attribute__((target("avx2"))) static void copy_nt_avx2(uint8_t *dst, const uint8_t *src, size_t n) {
+  size_t i = 0;
+  const size_t head = (32 - ((uintptr_t)dst & 31)) & 31;
+  if (head) {
+    const size_t h = head < n ? head : n;
+    memcpy(dst, src, h);
+    i = h;
+  }
+  for (; i + 128 <= n; i += 128) {
+    const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(src + i));
+    const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(src + i + 32));
+    const __m256i c = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(src + i + 64));
+    const __m256i d = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(src + i + 96));
+    _mm256_stream_si256(reinterpret_cast<__m256i *>(dst + i), a);
+    _mm256_stream_si256(reinterpret_cast<__m256i *>(dst + i + 32), b);
+    _mm256_stream_si256(reinterpret_cast<__m256i *>(dst + i + 64), c);
+    _mm256_stream_si256(reinterpret_cast<__m256i *>(dst + i + 96), d);
+  }
+  if (i < n) memcpy(dst + i, src + i, n - i);
+  _mm_sfence();
+}
+
+void copy_to_staging(void *dst, const void *src, size_t n) {
+  static const bool avx2 = __builtin_cpu_supports("avx2") && getenv("ZT_NO_NT_COPY") == nullptr;
+  if (avx2 && n >= 4096)
+    copy_nt_avx2(static_cast<uint8_t *>(dst), static_cast<const uint8_t *>(src), n);
+  else if (n)
+    memcpy(dst, src, n);
+}
+
+// copy threads of parallel_copy on this thread (the batch's device threads
+// split the host's copy threads between them: set_copy_threads)
+static thread_local size_t tl_copy_threads = 8;
+void set_copy_threads(size_t k) { tl_copy_threads = k < 1 ? 1 : k; }
+
 void parallel_copy(size_t count, const std::function<void(size_t)> &fn, size_t total_bytes) {
-  // host memcpy fan-out for the batch paths: one thread per ~8 MiB, at most 8
+  // host memcpy fan-out for the batch paths: one thread per ~8 MiB, at most
+  // tl_copy_threads (8 unless a multi-device batch shares them out)
   size_t nt = total_bytes >> 23;
-  if (nt > 8) nt = 8;
+  if (nt > tl_copy_threads) nt = tl_copy_threads;
   if (nt > count) nt = count;
   if (nt < 2) {
     for (size_t i = 0; i < count; ++i) fn(i);

@@ -52,11 +52,11 @@ struct DeviceCtx {
   uint32_t *d_crc_shift = nullptr;  // checksum.hip merge constants (crc_shift_tables)
   CkAcc *d_ck_acc = nullptr;        // checksum merge accumulators (zeroed once, left zeroed by every call)
   // scratch
-  static constexpr int kSlots = 27;
+  static constexpr int kSlots = 28;
   void *d_buf[kSlots] = {};  // slot 8: checksum segment partials; 10-17: general inflate (inflate_gen.hip);
                              // 20: segment inflate's sync-point sort (inflate_seg.hip); 21: stored runs;
                              // 22: pipelined host inflate's output, 23-25: its overflow ring (inflate_api.cpp);
-                             // 26: general inflate's window pointer-jumping buffers
+                             // 26: general inflate's window pointer-jumping buffers; 27: framed batch members
   size_t buf_size[kSlots] = {};
   // second stream: checksums run beside the deflate pipeline in the containers
   hipStream_t aux = nullptr;
@@ -118,10 +118,25 @@ bool host_direct(const void *p, size_t n);
 // One host allocation for `items` batch outputs (pointers inside it, each
 // released by zt_free; reserve >= 1 byte per item so every pointer is
 // distinct).  slab_release: true when p lay in a slab (and was released).
-uint8_t *slab_out(size_t total, size_t items);
+uint8_t *slab_out(size_t total, size_t items, bool pool = false);
+// device framing of batch members (synth.hip): item k's prefix | body |
+// trailer at out + it[k].out_off; trailer 8 = gzip (CRC-32 LE, ISIZE LE),
+// 4 = zlib (Adler-32 BE), 0 = none; sums = (crc, adler) per item
+struct FrameItem {
+  uint64_t body_off;  // in the deflate output
+  uint64_t out_off;   // in the framed output
+  uint32_t body_len;
+  uint32_t isize;
+};
+int frame_members_dev(const FrameItem *d_items, uint32_t count, const uint8_t *d_prefix, uint32_t plen,
+                      uint32_t trailer, const uint8_t *d_body, const uint32_t *d_sums, uint8_t *d_out, hipStream_t s);
 bool slab_release(void *p);
 // fn(0 .. count-1) over a few host threads when total_bytes is large.
+// memcpy into pinned staging with streaming stores (zt_api.cpp)
+void copy_to_staging(void *dst, const void *src, size_t n);
 void parallel_copy(size_t count, const std::function<void(size_t)> &fn, size_t total_bytes);
+// parallel_copy's thread budget on the calling thread (default 8)
+void set_copy_threads(size_t k);
 
 // ---- CRC-32 algebra (reflected, P = 0xEDB88320) ------------------------------
 // Host and device copies of zlib-style polynomial arithmetic: shifting a raw
