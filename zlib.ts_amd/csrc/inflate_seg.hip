@@ -86,6 +86,15 @@ __device__ __forceinline__ uint32_t fs_word(const uint8_t *in, uint64_t n, int64
 #endif
 constexpr uint32_t FS_ITER = ZT_FS_ITER;  // 4 KiB spans per workgroup (fewer, longer workgroups)
 constexpr uint32_t kFsLocal = 64;  // sync candidates a workgroup gathers before its one global atomic
+// Workgroup k appends to list region k % FS_SPLIT (its own counter, in its own
+// 128-byte line): one counter took every workgroup's atomic, serialised where
+// device-scope atomics execute; fs_gather then packs the regions
+#ifndef ZT_FS_SPLIT
+#define ZT_FS_SPLIT 64
+#endif
+constexpr uint32_t FS_SPLIT = ZT_FS_SPLIT;
+constexpr uint32_t kFsRegion = kMaxSync / FS_SPLIT;  // candidates per region (more: the stream leaves this path)
+constexpr uint32_t kFsCountStride = 32;             // u32 counters 128 bytes apart
 #ifndef ZT_FS_NT
 #define ZT_FS_NT 1
 #endif
@@ -93,28 +102,52 @@ __global__ __launch_bounds__(256) void find_syncs(const uint8_t *__restrict__ in
                                                   uint64_t *__restrict__ list, uint32_t *__restrict__ count) {
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
   const int lane = threadIdx.x & 63;
+  uint32_t *rcount = count + (blockIdx.x % FS_SPLIT) * kFsCountStride;
+  uint64_t *rlist = list + (uint64_t)(blockIdx.x % FS_SPLIT) * kFsRegion;
   __shared__ uint32_t s_n, s_base;
   __shared__ uint64_t s_list[kFsLocal];
   if (threadIdx.x == 0) s_n = 0;
   __syncthreads();
-  // every span's 16-byte load in flight before the first is scanned
+  // A wave scans FS_ITER contiguous KiB (1 KiB per step, 16 bytes per lane):
+  // the bytes around a lane's chunk come from its neighbours, across steps
+  // from the previous step's lane 63 / the next step's lane 0, and only the
+  // wave's two ends are loaded apart -- with the chunks, all in flight at once
+  const uint32_t wv = threadIdx.x >> 6;
+  const uint64_t wbase = (lo & ~uint64_t(15)) + ((uint64_t)blockIdx.x * FS_ITER * 256 + (uint64_t)wv * FS_ITER * 64) * 16;
+  const bool in16 = (reinterpret_cast<uintptr_t>(in) & 15) == 0;
+  const bool aligned = (reinterpret_cast<uintptr_t>(in) & 3) == 0;
+  const uint32_t *in32 = reinterpret_cast<const uint32_t *>(in);
+  auto edge = [&](int64_t q) -> uint32_t {  // 4 bytes at q, as fs_word
+    return aligned && q >= 0 && (uint64_t)q + 4 <= n ? in32[q / 4] : fs_word(in, n, q);
+  };
   u32x4 pre[FS_ITER];
 #pragma unroll
   for (uint32_t it = 0; it < FS_ITER; ++it) {
-    const uint64_t base =
-        (lo & ~uint64_t(15)) + (((uint64_t)blockIdx.x * FS_ITER + it) * 256 + threadIdx.x) * 16;
-    pre[it] = base + 16 <= n && (reinterpret_cast<uintptr_t>(in) & 15) == 0
+    const uint64_t base = wbase + ((uint64_t)it * 64 + lane) * 16;
+    pre[it] = base + 16 <= n && in16
                   ? (ZT_FS_NT ? __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(in + base))
                              : *reinterpret_cast<const u32x4 *>(in + base))
                   : u32x4{0u, 0u, 0u, 0u};
   }
+  // lane 0: the 8 bytes before the wave's span; lane 63: the 12 after it
+  uint32_t e0 = 0, e1 = 0, e2 = 0;
+  if (lane == 0) {
+    e0 = edge((int64_t)wbase - 8);
+    e1 = edge((int64_t)wbase - 4);
+  }
+  if (lane == 63) {
+    const int64_t q = (int64_t)(wbase + (uint64_t)FS_ITER * 1024);
+    e0 = edge(q);
+    e1 = edge(q + 4);
+    e2 = edge(q + 8);
+  }
+  uint32_t c0 = e0, c1 = e1;  // lane 0: the 8 bytes before this step's chunk
 #pragma unroll
   for (uint32_t it = 0; it < FS_ITER; ++it) {
-  const uint64_t base =
-      (lo & ~uint64_t(15)) + (((uint64_t)blockIdx.x * FS_ITER + it) * 256 + threadIdx.x) * 16;
+  const uint64_t base = wbase + ((uint64_t)it * 64 + lane) * 16;
   // words: w[0..1] = bytes [base - 8, base), w[2..5] = [base, base + 16), w[6..8] = [base + 16, base + 28)
   uint32_t w[9];
-  const bool whole = base + 16 <= n && (reinterpret_cast<uintptr_t>(in) & 15) == 0;
+  const bool whole = base + 16 <= n && in16;
   if (whole) {
     const u32x4 v = pre[it];
     w[2] = v.x;
@@ -130,18 +163,28 @@ __global__ __launch_bounds__(256) void find_syncs(const uint8_t *__restrict__ in
   w[6] = (uint32_t)__shfl_down((int)w[2], 1, 64);
   w[7] = (uint32_t)__shfl_down((int)w[3], 1, 64);
   w[8] = (uint32_t)__shfl_down((int)w[4], 1, 64);
-  const bool aligned = (reinterpret_cast<uintptr_t>(in) & 3) == 0;
-  const uint32_t *in32 = reinterpret_cast<const uint32_t *>(in);
   if (lane == 0) {
-    const bool ok = aligned && base >= 8 && base <= n;
-    w[0] = ok ? in32[(base - 8) / 4] : fs_word(in, n, (int64_t)base - 8);
-    w[1] = ok ? in32[(base - 4) / 4] : fs_word(in, n, (int64_t)base - 4);
+    w[0] = c0;
+    w[1] = c1;
   }
-  if (lane == 63) {
-    const bool ok = aligned && base + 28 <= n;
-    w[6] = ok ? in32[(base + 16) / 4] : fs_word(in, n, (int64_t)base + 16);
-    w[7] = ok ? in32[(base + 20) / 4] : fs_word(in, n, (int64_t)base + 20);
-    w[8] = ok ? in32[(base + 24) / 4] : fs_word(in, n, (int64_t)base + 24);
+  c0 = (uint32_t)__builtin_amdgcn_readlane((int)w[4], 63);
+  c1 = (uint32_t)__builtin_amdgcn_readlane((int)w[5], 63);
+  if (it + 1 < FS_ITER) {
+    // the next step's first 12 bytes: lane 0's chunk there when it is whole
+    const uint64_t nb = wbase + (uint64_t)(it + 1) * 1024;
+    const bool nwhole = nb + 16 <= n && in16;
+    const uint32_t x0 = (uint32_t)__builtin_amdgcn_readlane((int)pre[it + 1].x, 0);
+    const uint32_t x1 = (uint32_t)__builtin_amdgcn_readlane((int)pre[it + 1].y, 0);
+    const uint32_t x2 = (uint32_t)__builtin_amdgcn_readlane((int)pre[it + 1].z, 0);
+    if (lane == 63) {
+      w[6] = nwhole ? x0 : fs_word(in, n, (int64_t)nb);
+      w[7] = nwhole ? x1 : fs_word(in, n, (int64_t)nb + 4);
+      w[8] = nwhole ? x2 : fs_word(in, n, (int64_t)nb + 8);
+    }
+  } else if (lane == 63) {
+    w[6] = e0;
+    w[7] = e1;
+    w[8] = e2;
   }
   if (base >= n) continue;
   auto at = [&](int x) -> uint32_t {  // 4 bytes at base - 8 + x (0 <= x <= 32)
@@ -154,15 +197,14 @@ __global__ __launch_bounds__(256) void find_syncs(const uint8_t *__restrict__ in
       if (p > lo && p < n) {
         // bytes base + j - 6 .. base + j - 1: 00 00 00 FF FF 00
         const bool restart = base + j >= 6 && at(2 + j) == 0xFF000000u && (at(6 + j) & 0xFFFFu) == 0x00FFu;
-        // gathered per workgroup (one global atomic per workgroup: hits
-        // from every workgroup on one counter serialise at its L2 slice)
+        // gathered per workgroup (one global atomic per workgroup)
         const uint64_t v = (p << 1) | (restart ? 1 : 0);
         const uint32_t k = atomicAdd(&s_n, 1u);
         if (k < kFsLocal) {
           s_list[k] = v;
         } else {
-          const uint32_t g = atomicAdd(count, 1u);
-          if (g < kMaxSync) list[g] = v;
+          const uint32_t g = atomicAdd(rcount, 1u);
+          if (g < kFsRegion) rlist[g] = v;
         }
       }
     }
@@ -170,10 +212,43 @@ __global__ __launch_bounds__(256) void find_syncs(const uint8_t *__restrict__ in
   }
   __syncthreads();
   const uint32_t m = s_n < kFsLocal ? s_n : kFsLocal;
-  if (threadIdx.x == 0 && m) s_base = atomicAdd(count, m);
+  if (threadIdx.x == 0 && m) s_base = atomicAdd(rcount, m);
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < m; i += 256)
-    if (s_base + i < kMaxSync) list[s_base + i] = s_list[i];
+    if (s_base + i < kFsRegion) rlist[s_base + i] = s_list[i];
+}
+
+// the FS_SPLIT regions of find_syncs packed into `out` (region order; the
+// sort that follows makes the order irrelevant), one workgroup per region;
+// *total = the candidates, or kMaxSync + 1 when a region overflowed
+__global__ __launch_bounds__(256) void fs_gather(const uint64_t *__restrict__ list, const uint32_t *__restrict__ count,
+                                                 uint64_t *__restrict__ out, uint32_t *__restrict__ total) {
+  const uint32_t r = blockIdx.x;
+  __shared__ uint32_t s_off, s_over;
+  if (threadIdx.x < 64) {
+    uint32_t below = 0, all = 0, over = 0;
+    for (uint32_t q = threadIdx.x; q < FS_SPLIT; q += 64) {
+      const uint32_t c = count[q * kFsCountStride];
+      over |= c > kFsRegion ? 1u : 0u;
+      all += c;
+      below += q < r ? c : 0u;
+    }
+    for (int o = 32; o; o >>= 1) {
+      below += (uint32_t)__shfl_xor((int)below, o, 64);
+      all += (uint32_t)__shfl_xor((int)all, o, 64);
+      over |= (uint32_t)__shfl_xor((int)over, o, 64);
+    }
+    if (threadIdx.x == 0) {
+      s_off = below;
+      s_over = over;
+      if (r == 0) *total = over ? kMaxSync + 1 : all;
+    }
+  }
+  __syncthreads();
+  if (s_over) return;
+  const uint32_t c = count[r * kFsCountStride];
+  const uint64_t *src = list + (uint64_t)r * kFsRegion;
+  for (uint32_t i = threadIdx.x; i < c; i += 256) out[s_off + i] = src[i];
 }
 
 size_t align256(size_t v) { return (v + 255) & ~size_t(255); }
@@ -510,14 +585,20 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   if (n < index + (1u << 14)) return 1;  // small: one wave is as fast
   // 1. sync points
   void *d_cand;
-  ZT_TRY(scratch(c, 5, 256 + (size_t)kMaxSync * 8, &d_cand));
-  uint32_t *d_count = static_cast<uint32_t *>(d_cand);
-  uint64_t *d_list = reinterpret_cast<uint64_t *>(static_cast<uint8_t *>(d_cand) + 256);
-  ZT_HIP(hipMemsetAsync(d_count, 0, 4, s));
+  // [counters: FS_SPLIT lines | total][regions: kMaxSync][packed: kMaxSync]
+  constexpr size_t kCntBytes = (size_t)FS_SPLIT * kFsCountStride * 4 + 256;
+  ZT_TRY(scratch(c, 5, kCntBytes + 2 * (size_t)kMaxSync * 8, &d_cand));
+  uint32_t *d_rcount = static_cast<uint32_t *>(d_cand);
+  uint32_t *d_count = d_rcount + (size_t)FS_SPLIT * kFsCountStride;
+  uint64_t *d_regions = reinterpret_cast<uint64_t *>(static_cast<uint8_t *>(d_cand) + kCntBytes);
+  uint64_t *d_list = d_regions + kMaxSync;
+  ZT_HIP(hipMemsetAsync(d_rcount, 0, (size_t)FS_SPLIT * kFsCountStride * 4, s));
   const uint64_t span = n - (index & ~size_t(15));
   const uint32_t grid = (uint32_t)((span + 16 * 256 * FS_ITER - 1) / (16 * 256 * FS_ITER));
   ZT_TRY(timing_begin(c, s, 2));
-  find_syncs<<<grid, 256, 0, s>>>(d_in, index, n, d_list, d_count);
+  find_syncs<<<grid, 256, 0, s>>>(d_in, index, n, d_regions, d_rcount);
+  ZT_HIP(hipGetLastError());
+  fs_gather<<<FS_SPLIT, 256, 0, s>>>(d_regions, d_rcount, d_list, d_count);
   ZT_HIP(hipGetLastError());
   uint32_t cnt = 0;
   ZT_TRY(readback(c, &cnt, d_count, 4, s));
