@@ -579,31 +579,74 @@ __global__ __launch_bounds__(CK_THREADS, ZT_CK_MINW) void checksum_segments(cons
     }
     __syncthreads();
   }
-  if (fin.acc && tid == 0) {
+  if (fin.acc) {
     // CRC32.update: ~(shift(~crc_in, n) ^ raw); Adler32.update below
-    if (DO_CRC && blockIdx.x == 0) wg_crc ^= shift_bytes(shift_g + ZT_CRC_DIG_OFF, x2n, fin.n, ~fin.crc_in);
+    if (DO_CRC && blockIdx.x == 0 && tid == 0) wg_crc ^= shift_bytes(shift_g + ZT_CRC_DIG_OFF, x2n, fin.n, ~fin.crc_in);
     // Device-scope atomics are performed past the XCD's L2, and a returned
-    // value means this one has been: the done count is bumped only after the
-    // three sums have landed, so no __threadfence (an L2 write-back +
-    // invalidate per workgroup, which made the kernel 0.223 -> 0.258 ms)
+    // value means this one has been: a workgroup's partial sums go to its own
+    // slot by exchanges, and its ticket is taken only after they returned (no
+    // __threadfence: an L2 write-back + invalidate per workgroup, which made
+    // the kernel 0.223 -> 0.258 ms).  Tickets: one per group of workgroups
+    // (128 bytes apart), the group's last takes the top one -- one counter for
+    // every workgroup serialised ~1 K same-address atomics at the kernel's end
     CkAcc *a = fin.acc;
-    uint32_t landed = 0;
-    if (DO_CRC) landed ^= atomicXor(&a->crc, wg_crc);
-    if (DO_ADLER) {
-      landed ^= (uint32_t)atomicAdd(&a->s1, (unsigned long long)wg_s1);
-      landed ^= (uint32_t)atomicAdd(&a->s2, (unsigned long long)wg_s2);
+    __shared__ uint32_t s_last;
+    if (tid == 0) {
+      CkPart *pp = &a->part[blockIdx.x];
+      uint32_t landed = atomicExch(&pp->crc, wg_crc);
+      landed ^= (uint32_t)atomicExch(&pp->s1, (unsigned long long)wg_s1);
+      landed ^= (uint32_t)atomicExch(&pp->s2, (unsigned long long)wg_s2);
+      asm volatile("" ::"v"(landed) : "memory");  // waits for the returns
+      const uint32_t G = gridDim.x < (uint32_t)kCkGroups ? gridDim.x : (uint32_t)kCkGroups;
+      const uint32_t g = blockIdx.x % G;
+      const uint32_t members = (gridDim.x - g + G - 1) / G;
+      uint32_t last = 0;
+      if (atomicAdd(&a->grp[g * 32], 1u) == members - 1) {
+        atomicExch(&a->grp[g * 32], 0u);
+        last = atomicAdd(&a->done, 1u) == G - 1 ? 1u : 0u;
+      }
+      s_last = last;
     }
-    asm volatile("" ::"v"(landed) : "memory");  // waits for the returns
-    if (atomicAdd(&a->done, 1u) == gridDim.x - 1) {
-      const uint32_t raw = atomicExch(&a->crc, 0u);
-      const uint64_t r1 = atomicExch(&a->s1, 0ull) % 65521u, r2 = atomicExch(&a->s2, 0ull) % 65521u;
-      atomicExch(&a->done, 0u);
-      fin.result[0] = ~raw;
-      // s1 = adler & 0xFFFF, s2 = (adler >> 16) & 0xFFFF (need not be reduced)
-      const uint64_t a1 = fin.adler_in & 0xFFFFu, a2 = (fin.adler_in >> 16) & 0xFFFFu;
-      const uint64_t f1 = (a1 + r1) % 65521u;
-      const uint64_t f2 = (a2 + (fin.n % 65521u) * (a1 % 65521u) + r2) % 65521u;
-      fin.result[1] = (uint32_t)((f2 << 16) | f1);
+    __syncthreads();
+    if (s_last) {
+      // (read-modify-writes: the values at the point where the atomics landed)
+      uint32_t raw = 0;
+      unsigned long long r1 = 0, r2 = 0;
+      for (uint32_t w = tid; w < gridDim.x; w += CK_THREADS) {
+        CkPart *pp = &a->part[w];
+        raw ^= atomicOr(&pp->crc, 0u);
+        r1 += atomicAdd(&pp->s1, 0ull) % 65521u;
+        r2 += atomicAdd(&pp->s2, 0ull) % 65521u;
+      }
+      for (int off = 32; off > 0; off >>= 1) {
+        raw ^= (uint32_t)__shfl_xor((int)raw, off, 64);
+        r1 += __shfl_xor(r1, off, 64);
+        r2 += __shfl_xor(r2, off, 64);
+      }
+      if ((tid & 63) == 0) {
+        red_w[tid >> 6] = raw;
+        red_a[tid >> 6][0] = r1;
+        red_a[tid >> 6][1] = r2;
+      }
+      __syncthreads();
+      if (tid == 0) {
+        raw = 0;
+        r1 = r2 = 0;
+        for (int w = 0; w < CK_THREADS / 64; ++w) {
+          raw ^= red_w[w];
+          r1 += red_a[w][0];
+          r2 += red_a[w][1];
+        }
+        r1 %= 65521u;
+        r2 %= 65521u;
+        atomicExch(&a->done, 0u);
+        fin.result[0] = ~raw;
+        // s1 = adler & 0xFFFF, s2 = (adler >> 16) & 0xFFFF (need not be reduced)
+        const uint64_t a1 = fin.adler_in & 0xFFFFu, a2 = (fin.adler_in >> 16) & 0xFFFFu;
+        const uint64_t f1 = (a1 + r1) % 65521u;
+        const uint64_t f2 = (a2 + (fin.n % 65521u) * (a1 % 65521u) + r2) % 65521u;
+        fin.result[1] = (uint32_t)((f2 << 16) | f1);
+      }
     }
   }
 }
@@ -721,7 +764,9 @@ int checksums_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, bool do_crc, bool
   void *segbuf;
   ZT_TRY(scratch(c, 8, nseg * sizeof(SegResult), &segbuf));
   SegResult *segs = static_cast<SegResult *>(segbuf);
-  const int grid = (int)(nseg < (size_t)c->num_cu * 8 ? nseg : (size_t)c->num_cu * 8);
+  size_t g = nseg < (size_t)c->num_cu * 8 ? nseg : (size_t)c->num_cu * 8;
+  if (g > (size_t)kCkMaxWg) g = kCkMaxWg;  // (one partial slot per workgroup)
+  const int grid = (int)g;
   const CkFinish fin{c->d_ck_acc, d_result, n, crc_in, adler_in};
   if (do_crc && do_adler)
     checksum_segments<true, true><<<grid, CK_THREADS, 0, s>>>(frame, lo, hi, nseg, c->d_crc_nib, c->d_crc_x2n,

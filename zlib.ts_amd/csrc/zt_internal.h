@@ -31,9 +31,19 @@ int hip_fail(hipError_t e, const char *what);
 
 // ---- per-device context -----------------------------------------------------
 // checksum_segments' in-kernel merge (checksum.hip): zero between calls
-struct CkAcc {
+// checksum merge (checksum.hip): each workgroup's partial sums in its own
+// slot, then group tickets (128 bytes apart) and one top ticket -- the last
+// workgroup to arrive reduces the slots
+constexpr int kCkGroups = 32;
+constexpr int kCkMaxWg = 4096;  // checksums_dev's grid: at most num_cu * 8
+struct CkPart {
   unsigned long long s1, s2;
-  uint32_t crc, done;
+  uint32_t crc, pad[3];
+};
+struct CkAcc {
+  uint32_t grp[kCkGroups * 32];
+  uint32_t done, pad[31];
+  CkPart part[kCkMaxWg];
 };
 
 // One default stream per device plus grow-only scratch buffers, so the
