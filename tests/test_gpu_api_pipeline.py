@@ -3,7 +3,8 @@ restart-aligned pieces while earlier pieces are deflated and their streams
 come back (deflate_api.cpp deflate_raw_pipelined).  The pipelined call must
 write exactly the stream a single device-resident deflate of the whole
 buffer writes, and that stream must round-trip.  Sizes cover the threshold
-(64 MiB), a one-byte last piece and a piece count that is not a power of two.
+(64 MiB), a one-byte last piece, a piece count that is not a power of two and
+the growing pieces of inputs from 512 MiB.
 Reference: src/RawDeflate.ts:87-114 (one call, one stream).
 """
 import pytest
@@ -31,6 +32,7 @@ def _device_stream(zt, torch, d_in, n, level):
     ((64 << 20) + 1, 6, "mixed"),          # 3 pieces of 32 MiB, the last one byte
     ((160 << 20) + 12345, 6, "mixed"),     # 6 pieces, ragged last one
     (300 << 20, 1, "wordsalad"),           # 8 pieces of 38 MiB (rounded up to 1 MiB segments)
+    ((576 << 20) + 333, 6, "mixed"),       # the ramp from 512 MiB: 64, 128, 256, 128 MiB and 333 bytes
 ])
 def test_pipelined_deflate_equals_single_call(zt, n, level, kind):
     import numpy as np

@@ -16,6 +16,7 @@
 #   c4batch           C4 end to end                           (c4_batch.json)
 #   c4host            C4 host stages on 8 aliased devices     (c4_host_stages.json)
 #   api               host-API inflate time (appends)         (api.log)
+#   apid              host-API deflate time (appends)         (apid.log)
 #   infprof           rocprof kernel stats of infgen          (infgen_kernel_stats.csv)
 #   infgen[:MiB]      foreign-stream inflate timing           (inflate_general_time.json)
 #   infgenq           infgen, one summary line (appends)      (infgen.log)
@@ -63,6 +64,7 @@ for step in "$@"; do
     c4batch) timeout -k 10 300 python3 tools/c4_batch.py 10000 $O/c4_batch.json > $O/c4.log 2>&1; tail -3 $O/c4.log | cut -c1-300 ;;
     c4host) ZT_ALIAS_DEVICES=8 timeout -k 10 600 python3 tools/c4_host_stages.py 10000 $O/c4_host_stages.json > $O/c4_host_stages.log 2>&1; tail -5 $O/c4_host_stages.log ;;
     api) timeout -k 10 300 python3 tools/api_inflate_time.py >> $O/api.log 2>&1; echo "${ZT_LIB:-HEAD} $(tail -1 $O/api.log)" ;;
+    apid) timeout -k 10 300 python3 tools/api_deflate_time.py >> $O/apid.log 2>&1; echo "${ZT_LIB:-HEAD} $(tail -1 $O/apid.log)" ;;
     infprof) prof infgen 600 -- python3 $R/tools/inflate_general_time.py 64 ;;
     infgen) timeout -k 10 600 python3 -u tools/inflate_general_time.py 64 $O/inflate_general_time.json > $O/infgen.log 2>&1; tail -1 $O/infgen.log | cut -c1-600 ;;
     infgenq) timeout -k 10 600 python3 -u tools/inflate_general_time.py 64 $O/inflate_general_time.json >> $O/infgen.log 2>&1; echo "$(env | grep ZT_GEN | tr '\n' ' ') $(tail -1 $O/infgen.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print({k: (v["device"]["wall_ms"], v["device"]["passes_per_call"], v["host_api_GiBps"]) for k, v in d.items() if isinstance(v, dict)})')" ;;

@@ -108,33 +108,73 @@ int zt_deflate_dev(zt_deflate_plan *plan, const void *d_in, size_t n, size_t hal
 // match workgroups per CU and bound the fill / drain to one piece.
 static constexpr size_t kPipeMin = 64u << 20;
 
+// Piece sizes (whole segments).  From 512 MiB: 64, 128, then 256 MiB pieces
+// and the remainder -- a small first piece starts the deflate early, and
+// large pieces fill the GPU (a 128 MiB piece's one-wave-per-block kernels
+// leave it half empty: 4.1 ms per piece against 3.5 for an eighth of a 1 GiB
+// call); 1 GiB: 37.7 -> 34.8 ms (`gpurun_out/r06pc`, `r06pc2`,
+// tools/api_deflate_time.py).  Below: n / 8 clamped to 32..128 MiB.  Tuning
+// hook ZT_DF_PIECES = a list of MiB "a,b,c" (the last size repeats).
+static std::vector<size_t> deflate_pieces(size_t n, size_t seg) {
+  static const std::vector<size_t> env = [] {
+    std::vector<size_t> v;
+    if (const char *e = getenv("ZT_DF_PIECES"))
+      for (const char *q = e; *q;) {
+        char *end = nullptr;
+        const long x = strtol(q, &end, 10);
+        if (end == q) break;
+        if (x > 0) v.push_back((size_t)x << 20);
+        q = *end ? end + 1 : end;
+      }
+    return v;
+  }();
+  constexpr size_t MiB = 1u << 20;
+  std::vector<size_t> sched = env;
+  if (sched.empty()) {
+    if (n >= 512 * MiB)
+      sched = {64 * MiB, 128 * MiB, 256 * MiB};
+    else
+      sched = {std::min(std::max(n / 8, 32 * MiB), 128 * MiB)};
+  }
+  std::vector<size_t> sizes;
+  size_t off = 0;
+  for (size_t i = 0; off < n; ++i) {
+    size_t piece = sched[std::min(i, sched.size() - 1)];
+    piece = (piece + seg - 1) / seg * seg;
+    piece = std::min(piece, n - off);
+    sizes.push_back(piece);
+    off += piece;
+  }
+  return sizes;
+}
+
 static int deflate_raw_pipelined(DeviceCtx *c, const uint8_t *in, size_t n, int ct, int lv, uint8_t **out,
                                  size_t *out_len) {
-  const size_t seg = deflate_segment_bytes();
-  size_t piece = std::min(std::max(n / 8, (size_t)32 << 20), (size_t)128 << 20);
-  piece = (piece + seg - 1) / seg * seg;
-  const size_t np = (n + piece - 1) / piece;
-  const size_t pb = (out_bound(ct, piece) + 255) & ~(size_t)255;
+  const std::vector<size_t> sizes = deflate_pieces(n, deflate_segment_bytes());
+  const size_t np = sizes.size();
+  std::vector<size_t> in_off(np + 1, 0), out_off(np + 1, 0);
+  size_t pmax = 0;
+  for (size_t i = 0; i < np; ++i) {
+    in_off[i + 1] = in_off[i] + sizes[i];
+    out_off[i + 1] = out_off[i] + ((out_bound(ct, sizes[i]) + 255) & ~(size_t)255);
+    pmax = std::max(pmax, sizes[i]);
+  }
   void *d_in, *d_out, *d_scr;
   ZT_TRY(scratch(c, 0, n + 64, &d_in));
-  ZT_TRY(scratch(c, 1, pb * np, &d_out));
-  const size_t ss = deflate_scratch_bytes(c, piece);
+  ZT_TRY(scratch(c, 1, out_off[np], &d_out));
+  const size_t ss = deflate_scratch_bytes(c, pmax);
   ZT_TRY(scratch(c, 3, ss, &d_scr));
   PipeOut po;
-  po.base = host_out(pb * np, true);
-  po.cap = pb * np;
+  po.base = host_out(out_off[np], true);
+  po.cap = out_off[np];
   if (!po.base) return set_error(ZT_E_NOMEM, "host allocation failed");
   const int rc = pipeline_h2d_d2h(
       c, np,
-      [&](size_t i) {
-        const size_t off = i * piece;
-        return PipePiece{in + off, (uint8_t *)d_in + off, std::min(piece, n - off)};
-      },
+      [&](size_t i) { return PipePiece{in + in_off[i], (uint8_t *)d_in + in_off[i], sizes[i]}; },
       [&](size_t i, const void **d_res, size_t *n_res) -> int {
-        const size_t off = i * piece;
-        uint8_t *d_o = (uint8_t *)d_out + i * pb;
-        ZT_TRY(deflate_dev_run(c, (const uint8_t *)d_in + off, std::min(piece, n - off), 0, i + 1 == np, ct, lv, d_o,
-                               n_res, d_scr, ss, c->stream));
+        uint8_t *d_o = (uint8_t *)d_out + out_off[i];
+        ZT_TRY(deflate_dev_run(c, (const uint8_t *)d_in + in_off[i], sizes[i], 0, i + 1 == np, ct, lv, d_o, n_res,
+                               d_scr, ss, c->stream));
         *d_res = d_o;
         return ZT_OK;
       },
