@@ -323,15 +323,25 @@ static int inflate_host_batch(const uint8_t *const *in, const size_t *n, const s
   }
   void *d_in;
   ZT_TRY(scratch(c, 0, in_total, &d_in));
-  // inputs packed into pinned staging, one H2D copy
+  // inputs packed into pinned staging in chunks of about 32 MiB, each
+  // chunk's upload issued as soon as it is packed: the copy engine moves
+  // chunk k while the host packs chunk k + 1 (C2: pack 2.0 ms, then H2D 2.8)
   {
     void *h;
     ZT_TRY(pinned(c, in_total, &h));
     uint8_t *stage = (uint8_t *)h;
     BT("pack start");
-    parallel_copy(count, [&](size_t i) { copy_to_staging(stage + in_off[i], in[i], n[i]); }, in_total);
+    constexpr size_t kChunk = 32u << 20;
+    for (size_t a = 0; a < count;) {
+      size_t b = a + 1;
+      while (b < count && in_off[b] - in_off[a] < kChunk) ++b;
+      const size_t lo = in_off[a], hi = b < count ? in_off[b] : in_total;
+      // (every chunk with the whole batch's copy threads)
+      parallel_copy(b - a, [&](size_t k) { copy_to_staging(stage + in_off[a + k], in[a + k], n[a + k]); }, in_total);
+      ZT_HIP(hipMemcpyAsync((uint8_t *)d_in + lo, stage + lo, hi - lo, hipMemcpyHostToDevice, c->stream));
+      a = b;
+    }
     BT("pack done");
-    ZT_HIP(hipMemcpyAsync(d_in, stage, in_total, hipMemcpyHostToDevice, c->stream));
   }
   return inflate_dev_batch(c, d_in, in_off, n, index, count, strict, out, out_len, end_ip, status);
 }
