@@ -148,9 +148,11 @@ int scratch(DeviceCtx *c, int slot, size_t bytes, void **ptr) {
 // uploads from it (a stream handed back to zt_inflate_raw) go by DMA with no
 // pinned staging, host memcpy or page faults.  The free buffers the pool
 // keeps are bounded by ZT_HOST_POOL_MB (default 4096; 0: no pool, every
-// output freshly allocated); zt_release_scratch drops them.  Batch and
-// container outputs are not pooled (one-shot callers would pay the
-// registration for nothing).
+// output freshly allocated); zt_release_scratch drops them.  The batch
+// calls' slabs (slab_out: the GZip batch's framed members, the batch
+// inflate's outputs) come from the pool too -- a slab returns once its last
+// item is freed -- so a batch caller in a loop downloads by DMA straight
+// into them (C2: 22.7 -> 15.7 ms per 4096 x 64 KiB).
 static uint8_t *host_alloc(size_t n) {
   // 2 MiB-aligned and backed by transparent huge pages where the kernel
   // allows it -- 512x fewer first-touch faults while the download fills them
