@@ -273,9 +273,17 @@ __global__ __launch_bounds__(256) void unit_jobs(const uint64_t *__restrict__ ke
                                                  const uint32_t *__restrict__ pos, uint32_t cnt, uint64_t n,
                                                  uint64_t index, uint32_t cap, uint64_t *__restrict__ sync,
                                                  uint8_t *__restrict__ restart, TokJob *__restrict__ jobs,
-                                                 uint64_t *__restrict__ slot, uint32_t *__restrict__ nrestart) {
+                                                 uint64_t *__restrict__ slot, uint32_t *__restrict__ nrestart,
+                                                 uint32_t *__restrict__ span_key, uint32_t *__restrict__ unit_id) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   auto job = [&](uint32_t u, uint64_t start, uint64_t next) {
+    // (launch order: the longest input span first -- sorted on a 20-bit
+    // key, spans of 1 MiB and more tied first)
+    const uint64_t span = next > start ? next - start : 0;
+    if (span_key) {
+      span_key[u] = 0xFFFFFu - (uint32_t)(span < 0xFFFFFull ? span : 0xFFFFFull);
+      unit_id[u] = u;
+    }
     TokJob j;
     j.start = start;
     j.tok_off = 0;  // unit_slots
@@ -647,8 +655,26 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
       reinterpret_cast<TokResult *>(static_cast<uint8_t *>(d_meta) + stops_bytes + restart_bytes + jobs_bytes);
   ZT_HIP(hipMemsetAsync(d_slot, 0, units_max * 8, s));
   ZT_HIP(hipMemsetAsync(d_ttot + 2, 0, 8, s));
+  // tokenize launch order (slot 28): [span keys | unit ids | sorted keys |
+  // sorted ids | sort storage]
+  // (up to 128 K candidates: 4 GiB of 32 KiB blocks; a crafted stream of
+  // dense false candidates keeps the position order and no order buffers)
+  static const bool lpt_env = getenv("ZT_TOK_ORDER") ? atoi(getenv("ZT_TOK_ORDER")) != 0 : true;
+  const bool lpt = lpt_env && units_max <= (1u << 17);
+  size_t t_ord = 0;
+  if (lpt)
+    ZT_HIP(rocprim::radix_sort_pairs(nullptr, t_ord, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                     (const uint32_t *)nullptr, (uint32_t *)nullptr, units_max, 0u, 20u, s));
+  const size_t ord_b = align256((lpt ? units_max : 1) * 4);
+  void *d_ordbuf;
+  ZT_TRY(scratch(c, 28, 4 * ord_b + align256(t_ord), &d_ordbuf));
+  uint32_t *d_skey = static_cast<uint32_t *>(d_ordbuf);
+  uint32_t *d_uid = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(d_ordbuf) + ord_b);
+  uint32_t *d_skey2 = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(d_ordbuf) + 2 * ord_b);
+  uint32_t *d_order = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(d_ordbuf) + 3 * ord_b);
+  void *d_ordtmp = static_cast<uint8_t *>(d_ordbuf) + 4 * ord_b;
   unit_jobs<<<g, 256, 0, s>>>(d_key, d_flag, d_pos, cnt, n, index, kUnitTokCap, d_stops, d_restart, d_jobs, d_slot,
-                              reinterpret_cast<uint32_t *>(d_ttot + 2));
+                              reinterpret_cast<uint32_t *>(d_ttot + 2), lpt ? d_skey : nullptr, d_uid);
   ZT_HIP(hipGetLastError());
   ZT_HIP(rocprim::exclusive_scan(sb, t_scan64, d_slot, d_off, (uint64_t)0, units_max, rocprim::plus<uint64_t>(), s));
   unit_slots<<<g, 256, 0, s>>>(d_off, d_slot, d_pos + cnt, d_jobs, d_ttot);
@@ -692,9 +718,14 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
   ZT_TRY(pinned(c, meta_a + meta_b, &hp, 1));
   uint8_t *pin = static_cast<uint8_t *>(hp);
   const uint8_t *restart = pin;
+  // longest units first: the kernel's last units are short ones, so its tail
+  // (SIMDs idle while the last units finish) is short
+  if (lpt && units > 1)
+    ZT_HIP(rocprim::radix_sort_pairs(d_ordtmp, t_ord, d_skey, d_skey2, d_uid, d_order, units, 0u, 20u, s));
   TokParams tp;
   tp.in = d_in;
   tp.n = n;
+  tp.order = lpt && units > 1 ? d_order : nullptr;
   tp.stops = d_stops;
   tp.nstops = nsync;
   tp.jobs = d_jobs;

@@ -51,7 +51,7 @@ struct TokShared {
 __global__ __launch_bounds__(64) ZT_TOK_ATTR void tokenize_kernel(TokParams P) {
   __shared__ TokShared sh;
   __shared__ SpecShared spsh;
-  const uint32_t u = blockIdx.x;
+  const uint32_t u = P.order ? P.order[blockIdx.x] : blockIdx.x;
   const int lane = threadIdx.x & 63;
   const TokJob job = P.jobs[u];
   const uint64_t n = job.end ? job.end : P.n;

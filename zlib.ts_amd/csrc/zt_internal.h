@@ -62,11 +62,12 @@ struct DeviceCtx {
   uint32_t *d_crc_shift = nullptr;  // checksum.hip merge constants (crc_shift_tables)
   CkAcc *d_ck_acc = nullptr;        // checksum merge accumulators (zeroed once, left zeroed by every call)
   // scratch
-  static constexpr int kSlots = 28;
+  static constexpr int kSlots = 29;
   void *d_buf[kSlots] = {};  // slot 8: checksum segment partials; 10-17: general inflate (inflate_gen.hip);
                              // 20: segment inflate's sync-point sort (inflate_seg.hip); 21: stored runs;
                              // 22: pipelined host inflate's output, 23-25: its overflow ring (inflate_api.cpp);
-                             // 26: general inflate's window pointer-jumping buffers; 27: framed batch members
+                             // 26: general inflate's window pointer-jumping buffers; 27: framed batch members;
+                             // 28: segment inflate's tokenize launch order
   size_t buf_size[kSlots] = {};
   // second stream: checksums run beside the deflate pipeline in the containers
   hipStream_t aux = nullptr;
@@ -289,6 +290,7 @@ struct TokResult {
 struct TokParams {
   const uint8_t *in;
   uint64_t n;
+  const uint32_t *order;  // workgroup g decodes unit order[g] (null: unit g)
   const uint64_t *stops;  // sorted sync points
   uint64_t nstops;
   const TokJob *jobs;
