@@ -383,7 +383,8 @@ __global__ __launch_bounds__(CH_T) void chain_kernel(const TokResult *__restrict
                                                      const uint64_t *__restrict__ tok_off, uint32_t units,
                                                      uint64_t out_cap, uint64_t desc_cap, uint32_t max_seg,
                                                      ChainUnit *__restrict__ cu, SegJob *__restrict__ sj,
-                                                     ChainInfo *__restrict__ info) {
+                                                     ChainInfo *__restrict__ info, uint32_t *__restrict__ ekey,
+                                                     uint32_t *__restrict__ eid) {
   __shared__ uint16_t ol[CH_MAXU];              // unit output bytes (<= 65535 here)
   __shared__ uint32_t candb[CH_MAXU / 32];      // unit follows a restart point (or is unit 0)
   __shared__ uint32_t dirb[CH_MAXU / 32];       // unit is stored runs only, or empty
@@ -555,6 +556,11 @@ __global__ __launch_bounds__(CH_T) void chain_kernel(const TokResult *__restrict
         x.ntok = seg_direct[g] ? nt[j] : (nt[j] & ~0x40000000u);
         x.out_len = l;
         cu[u] = x;
+        if (ekey) {  // expand's launch order: most tokens first (17-bit key)
+          const uint32_t nt = x.ntok & 0x3FFFFFFFu;
+          ekey[u] = 0x1FFFFu - (nt < 0x1FFFFu ? nt : 0x1FFFFu);
+          eid[u] = u;
+        }
       }
       k += (uint32_t)__popcll(sm);
     }
@@ -784,9 +790,12 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
                                                                                         boundary, d_bflag);
       ZT_HIP(hipGetLastError());
     }
+    // (the tokenize order's buffers, free again, hold expand's: most tokens first)
     chain_kernel<<<1, CH_T, 0, s>>>(d_res, d_restart, d_off, (uint32_t)units, out_cap, desc_cap, max_seg, d_cu, d_sj,
-                                    d_info);
+                                    d_info, lpt ? d_skey : nullptr, d_uid);
     ZT_HIP(hipGetLastError());
+    if (lpt && units > 1)
+      ZT_HIP(rocprim::radix_sort_pairs(d_ordtmp, t_ord, d_skey, d_skey2, d_uid, d_order, units, 0u, 20u, s));
     ResolveParams rp;
     rp.tokens = static_cast<const uint32_t *>(d_tok);
     rp.units = d_cu;
@@ -800,6 +809,7 @@ int inflate_segments_dev(DeviceCtx *c, const uint8_t *d_in, size_t n, size_t ind
     rp.marker = 0;
     rp.in = d_in;
     rp.info = d_info;
+    rp.order = lpt && units > 1 ? d_order : nullptr;
     IT("device chain launched");
     ZT_TRY(resolve_segments_dev(rp, s));
     ZT_TRY(timing_end(c, s, 2));

@@ -238,7 +238,7 @@ struct ExpandShared {
 // them take the loop without the run checks
 template <bool RUNS>
 __device__ __forceinline__ void expand_unit(const ResolveParams &P, ExpandShared &sh, const ChainUnit &cu) {
-  const uint32_t u = blockIdx.x;
+  const uint32_t u = P.order ? P.order[blockIdx.x] : blockIdx.x;
   const int lane = threadIdx.x & 63;
   const uint32_t *tk = P.tokens + cu.tok_off;
   const uint32_t ntok = cu.ntok & 0x3FFFFFFFu;
@@ -463,13 +463,13 @@ __device__ __forceinline__ void expand_direct(const ResolveParams &P, const Chai
     wave_copy(P.out + cu.out_off + op, P.in + src, rl, lane);
     op += rl;
   }
-  if (lane == 0) P.unit_status[blockIdx.x] = ok && op == cu.out_len ? ZT_OK : ZT_E_INPUT_BROKEN;
+  if (lane == 0) P.unit_status[P.order ? P.order[blockIdx.x] : blockIdx.x] = ok && op == cu.out_len ? ZT_OK : ZT_E_INPUT_BROKEN;
 }
 
 __global__ __launch_bounds__(64) void expand_kernel(ResolveParams P) {
   __shared__ ExpandShared sh;
   if (P.info && !P.info->ok) return;  // the host walks the chain instead
-  const ChainUnit cu = P.units[blockIdx.x];
+  const ChainUnit cu = P.units[P.order ? P.order[blockIdx.x] : blockIdx.x];
   if ((cu.ntok >> 30) == 3u)
     expand_direct(P, cu);
   else if (cu.ntok >> 31)

@@ -342,6 +342,7 @@ struct ResolveParams {
   int32_t marker;        // expand: segments after the first may reach up to 32 KiB behind their start
   const uint8_t *in;     // expand: the compressed input (payloads of run tokens)
   const ChainInfo *info = nullptr;  // device-built chain: nothing to do unless info->ok; nseg = info->nseg
+  const uint32_t *order = nullptr;  // expand: workgroup g takes unit order[g] (null: unit g)
 };
 int tokenize_units_dev(const TokParams &p, hipStream_t s);
 int resolve_segments_dev(const ResolveParams &p, hipStream_t s);
