@@ -1545,24 +1545,18 @@ __device__ __forceinline__ void parse_window(S *s, const DeflateParams &P, uint3
       exit = (uint32_t)__builtin_amdgcn_readlane((int)ptr, (int)entry);
     }
     const bool on = (path >> lane) & 1;
+    // one literal / length increment for every path lane, then the distances
+    // (the two branches issued one LDS atomic instruction each: parse 2.35 ->
+    // 2.29 ms, price 0.565 -> 0.554 per GiB, streams identical, gpurun_out/abH)
     if (on) {
-      uint32_t token;
-      if (L >= 3) {
-        token = (L << 16) | res_dist(r);
+      const bool mt = L >= 3;
+      const uint32_t token = mt ? (L << 16) | res_dist(r) : res_byte(r);
+      lds_inc(&s->lit_hist[mt ? 257 + len_sym(L) : token]);
+      if (mt) {
         uint32_t eb, ev;
-#ifndef ZT_EXP_NOHIST
-        lds_inc(&s->lit_hist[257 + len_sym(L)]);
         lds_inc(&s->dist_hist[dist_sym(res_dist(r), eb, ev)]);
-#endif
-      } else {
-        token = res_byte(r);
-#ifndef ZT_EXP_NOHIST
-        lds_inc(&s->lit_hist[token]);
-#endif
       }
-#ifndef ZT_EXP_NOSTORE
       if (WRITE) r_blk[ntok + __popcll(path & lanemask_lt(lane))] = token;
-#endif
     }
     ntok += __popcll(path);
     entry = exit - 64;
@@ -1722,8 +1716,18 @@ __device__ __forceinline__ uint32_t op_price(uint32_t f, float inv_total) {
   return (uint32_t)(c < 8 ? 8 : c > 120 ? 120 : c);
 }
 
+// price sample: 1/ZT_PRICE_SAMPLE of each block in ZT_PRICE_PIECES pieces
+// spread over it.  The block's first 1/4 (sample 4, one piece) -> 1/8 in eight
+// 512-position pieces: price 0.55 -> 0.30 ms per GiB, streams smaller at
+// levels 6 and 9 (bench corpus at 128 MiB 0.53382 -> 0.53379), gate worst
+// 1.0193 -> 1.0191.  1/4 in 4 pieces: price unchanged, gate 1.0193; 1/8 in 4:
+// 0.29 ms, 1.0192; 1/16 in 4: 0.16 ms, 1.0197 (gpurun_out/abS4, abS8, abC,
+// abS16, abS8p8)
 #ifndef ZT_PRICE_SAMPLE
-#define ZT_PRICE_SAMPLE 4
+#define ZT_PRICE_SAMPLE 8
+#endif
+#ifndef ZT_PRICE_PIECES
+#define ZT_PRICE_PIECES 8
 #endif
 // greedy parse statistics -> prices (one wave per block, small LDS: many waves per CU)
 __global__ __launch_bounds__(64) void price_kernel(DeflateParams P) {
@@ -1738,10 +1742,19 @@ __global__ __launch_bounds__(64) void price_kernel(DeflateParams P) {
   for (int i = lane; i < 288; i += 64) s->lit_hist[i] = 0;
   if (lane < 32) s->dist_hist[lane] = 0;
   wsync();
-  // the prices only need symbol statistics: a greedy parse of the block's
-  // first 1/ZT_PRICE_SAMPLE (the full block when smaller) estimates them
+  // the prices only need symbol statistics: a greedy parse of 1/ZT_PRICE_SAMPLE
+  // of the block estimates them (a short block: its start, or all of it)
   const uint32_t plen = blen < (uint32_t)(DF_BLOCK / ZT_PRICE_SAMPLE) ? blen : (uint32_t)(DF_BLOCK / ZT_PRICE_SAMPLE);
-  parse_block<false>(s, &s->stage, P, P.res + lo, plen);
+  if (ZT_PRICE_PIECES > 1 && blen == DF_BLOCK) {
+    // the sample in ZT_PRICE_PIECES pieces spread over the block, each parsed
+    // greedily from its own start
+    constexpr uint32_t pl = DF_BLOCK / ZT_PRICE_SAMPLE / ZT_PRICE_PIECES;
+    static_assert(pl % (PB_CH * 64) == 0, "pieces take the LDS-DMA driver");
+    for (int j = 0; j < ZT_PRICE_PIECES; ++j)
+      parse_block<false>(s, &s->stage, P, P.res + lo + (uint64_t)j * (DF_BLOCK / ZT_PRICE_PIECES), pl);
+  } else {
+    parse_block<false>(s, &s->stage, P, P.res + lo, plen);
+  }
   wsync();
   BlockPrices *bp = reinterpret_cast<BlockPrices *>(P.slots + (size_t)blk * DF_SLOT);
   float tl = 0.f, td = 0.f;
